@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""RS(10,4) encode + reconstruct throughput on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over the whole per-GPU batch, device
+resident (inputs already in HBM when the timed region starts):
+  1. rs_encode_stripes: parity of every stripe (configs[1]: 6,553 stripes x
+     10 x 1 MiB shards = 64 GiB of data per GPU), and
+  2. rs_reconstruct_stripes: every stripe loses 1-4 random shards (uniform
+     count, uniform positions; a fresh erasure set per step, seed 0xE4A5),
+     which are regenerated in place (configs[2]), including the host-side
+     per-stripe pattern lookup and the stripe->pattern upload.
+value = algorithmic bytes of all steps on all ranks / max-over-ranks time,
+where encode moves (k+m)*S per stripe and reconstruct (k+e)*S.
+
+Multi-GPU (configs[3], stripe-local placement): each rank owns its own
+stripes (stripe s of the global job -> rank s mod N), no collective on the
+data path -> weak scaling.  The driver launches N>1 with torch.distributed.run.
+
+Also reported: the roofline of the dominant kernel (encode, HIP events on the
+launch stream) against the 8 TB/s HBM3E peak, and the CPU baseline (the
+oracle's AVX2 split-nibble port of infectious's addmul, on a bounded sample
+of the same workload, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "noise-erasurecode-plugin_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--n", type=int, default=14)
+    ap.add_argument("--shard", type=int, default=1 << 20, help="shard bytes S")
+    ap.add_argument("--stripes", type=int, default=6553, help="stripes per GPU")
+    ap.add_argument("--emin", type=int, default=1)
+    ap.add_argument("--emax", type=int, default=None)
+    ap.add_argument("--mode", choices=["both", "encode", "reconstruct"], default="both")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget of the CPU baseline sample (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def erasure_sets(rng, count, stripes, n, emin, emax):
+    out = []
+    for _ in range(count):
+        er = np.zeros((stripes, n), dtype=np.uint8)
+        es = rng.integers(emin, emax + 1, size=stripes)
+        for s in range(stripes):
+            er[s, rng.choice(n, size=int(es[s]), replace=False)] = 1
+        out.append(er)
+    return out
+
+
+def cpu_baseline(k, n, S, seconds, threads):
+    """Oracle on a bounded sample of the same workload: batches of RS(k, n)
+    stripes with S-byte shards, each batch encoded (AVX2 split-nibble port of
+    infectious's addmul) and then reconstructed from 1..m random erasures
+    (Rebuild per stripe), `threads` pthreads over stripes; same algorithmic
+    byte accounting as the GPU line.  Runs until `seconds` have elapsed."""
+    from oracle import oracle
+
+    m = n - k
+    E = oracle.fec_matrix(k, n)
+    batch = max(threads, 1)
+    data = oracle.splitmix_bytes(batch * k * S, 0xC0FFEE)
+    parity = np.zeros(batch * m * S, dtype=np.uint8)
+    rng = np.random.default_rng(0xE4A5)
+    done_bytes = 0
+    stripes_done = 0
+    busy = 0.0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        er = erasure_sets(rng, 1, batch, n, 1, m)[0]
+        a = time.perf_counter()
+        parity[:] = oracle.encode_batch(E, k, n, data, S, batch, simd=True, threads=threads)
+        rc = oracle.reconstruct_batch(E, k, n, data, parity, S, batch, er, simd=True,
+                                      threads=threads)
+        busy += time.perf_counter() - a
+        assert rc == 0
+        done_bytes += batch * (k + m) * S + int(((k + er.sum(axis=1)) * S).sum())
+        stripes_done += batch
+    return {
+        "value": round(done_bytes / busy / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{stripes_done} RS({k},{n}) stripes of {S} B shards, encode + 1-{m}-erasure "
+                  f"reconstruct (oracle/rs_oracle.c, AVX2 split-nibble addmul), {threads} "
+                  f"threads, {busy:.1f} s",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import rsmi
+
+    k, n, S = args.k, args.n, args.shard
+    m = n - k
+    emax = args.emax if args.emax is not None else m
+    stripes = args.stripes
+    f = rsmi.FEC(k, n, device=local)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device=dev)
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device=dev)
+    f.fill_splitmix(data.data_ptr(), data.numel(), 0x5EED ^ (rank << 32), sh)
+    f.fill_splitmix(parity.data_ptr(), parity.numel(), 1, sh)
+    f.prepare_patterns(emax, sh)
+    rng = np.random.default_rng(0xE4A5 + rank)
+    ersets = erasure_sets(rng, args.warmup + args.steps, stripes, n, args.emin, emax)
+    rec_bytes = [int(((k + er.sum(axis=1)) * S).sum()) for er in ersets]
+    enc_bytes = stripes * (k + m) * S
+
+    do_enc = args.mode in ("both", "encode")
+    do_rec = args.mode in ("both", "reconstruct")
+    if not do_enc:  # reconstruct needs valid parity once
+        f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, sh)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i, timed):
+        e = ev[i - args.warmup] if timed else None
+        if e:
+            e[0].record(stream)
+        if do_enc:
+            f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, sh)
+        if e:
+            e[1].record(stream)
+        if do_rec:
+            f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                                  ersets[i].tobytes(), sh)
+        if e:
+            e[2].record(stream)
+
+    for i in range(args.warmup):
+        step(i, False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i, True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = [a.elapsed_time(b) for a, b, _ in ev]
+    rec_ms = [b.elapsed_time(c) for _, b, c in ev]
+    step_bytes_local = sum((enc_bytes if do_enc else 0) + (rec_bytes[i] if do_rec else 0)
+                           for i in range(args.warmup, args.warmup + args.steps))
+    total_bytes = step_bytes_local * world
+    value = total_bytes / elapsed / 1e9
+
+    enc_avg_ms = sum(enc_ms) / len(enc_ms)
+    rec_avg_ms = sum(rec_ms) / len(rec_ms)
+    rec_avg_bytes = sum(rec_bytes[args.warmup:]) / args.steps
+    dominant = "encode" if do_enc else "reconstruct"
+    dom_bytes = enc_bytes if do_enc else rec_avg_bytes
+    dom_ms = enc_avg_ms if do_enc else rec_avg_ms
+    achieved = dom_bytes / (dom_ms / 1e3) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_json) as fh:
+            tj = json.load(fh)
+        key = f"{dominant}_k{k}_n{n}_S{S}_stripes{stripes}"
+        traffic = tj.get(key)
+    except (OSError, ValueError):
+        pass
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(k, n, S, args.cpu_seconds, thr)
+        out = {
+            "metric": "RS(10,4) encode+reconstruct GB/s at 1/8 GPUs; % HBM roofline",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes, device-generated; random 1-4 erasures/stripe)",
+            "config": {
+                "workload": f"RS({k},{n}) encode + {args.emin}-{emax}-erasure reconstruct of "
+                            f"{stripes} stripes x {k} x {S} B shards per GPU (configs[1]+[2])",
+                "k": k, "n": n, "shard_bytes": S, "stripes_per_gpu": stripes,
+                "data_bytes_per_gpu": stripes * k * S,
+                "parallelism": f"stripe-partitioned x{world}, no collective",
+                "mode": args.mode,
+            },
+            "breakdown": {
+                "encode_ms": round(enc_avg_ms, 3),
+                "encode_GBps": round(enc_bytes / (enc_avg_ms / 1e3) / 1e9, 1) if do_enc else None,
+                "encode_data_GBps": round(stripes * k * S / (enc_avg_ms / 1e3) / 1e9, 1) if do_enc else None,
+                "reconstruct_ms": round(rec_avg_ms, 3),
+                "reconstruct_GBps": round(rec_avg_bytes / (rec_avg_ms / 1e3) / 1e9, 1) if do_rec else None,
+                "reconstruct_frac": round(rec_avg_bytes / (rec_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if do_rec else None,
+                "kernel_variant": rsmi_variant(k, n),
+            },
+            "roofline": {
+                "kernel": f"rs_matmul_kernel ({dominant})",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": int(dom_bytes),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def rsmi_variant(k, n):
+    m = n - k
+    if k == 10 and m <= 4:
+        return "K10_MG4"
+    if k == 64 and m <= 16:
+        return "K64_MG16"
+    return "generic"
+
+
+if __name__ == "__main__":
+    main()

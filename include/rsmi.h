@@ -1,0 +1,138 @@
+/*
+ * rsmi.h -- C ABI of the MI355X-native Reed-Solomon engine that replaces the
+ * github.com/vivint/infectious calls on the shard encode/reconstruct path of
+ * da-moon/noise-erasurecode-plugin.
+ *
+ * Every entry point names the reference call site it replaces.  The Go side
+ * of the plugin (ShardPlugin, main.go:43-115/201-267) and the protobuf Shard
+ * message (protobuf/shard.proto:21-27) stay unchanged; a cgo package exposing
+ * NewFEC / (*FEC).Encode / (*FEC).Decode / Share on top of this header (see
+ * INTEGRATION.md) is the only change the plugin needs (its import at
+ * main.go:24).
+ *
+ * Conventions
+ *  - k = MinimumNeededShards (data shards), n = TotalShards, m = n - k.
+ *  - All arithmetic is GF(2^8), polynomial 0x11D, systematic Vandermonde code
+ *    with evaluation points {0, 2^1, ..., 2^(n-1)} (infectious NewFEC).
+ *  - Status codes are ints: RS_OK (0) or a negative rs_status.
+ *  - Host pointers are never retained past a call (cgo rule).
+ *  - Device pointers / streams are HIP device pointers / hipStream_t passed
+ *    as void*; the stream may be NULL (legacy default stream).
+ *  - An rs_ctx is bound to one HIP device; calls on one ctx are serialised by
+ *    an internal mutex, so a ctx may be shared between threads.
+ *  - There is no CPU fallback: without a usable gfx950 device rs_new returns
+ *    RS_EDEVICE.
+ */
+#ifndef RSMI_H
+#define RSMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    RS_OK = 0,
+    RS_EINVAL_KN = -1,         /* NewFEC: "requires 1 <= k <= n <= 256"            */
+    RS_ELEN_NOT_MULTIPLE = -2, /* Encode: "input length must be a multiple of k"   */
+    RS_ENOT_ENOUGH = -3,       /* Decode/Rebuild: NotEnoughShares                  */
+    RS_EBAD_SHARE_ID = -4,     /* Rebuild: "invalid share id"                      */
+    RS_ESINGULAR = -5,         /* invertMatrix: "singular matrix" (duplicate ids)  */
+    RS_ENO_SHARES = -6,        /* Decode: "must specify at least one share"        */
+    RS_ESHARE_LEN = -7,        /* shares of unequal length                         */
+    RS_EINVAL = -8,            /* bad argument (NULL, misaligned device buffer...) */
+    RS_EDEVICE = -9,           /* HIP runtime error or no gfx950 device            */
+    RS_ENOMEM = -10,           /* host or device allocation failed                 */
+} rs_status;
+
+typedef struct rs_ctx rs_ctx;
+
+/* ---- construction: replaces infectious.NewFEC(k, n) ---------------------
+ * main.go:73 (receive side, k/n from the message) and main.go:248 (send
+ * side, shardInput).  Builds the n x k systematic matrix once and uploads it;
+ * the plugin re-creating a ctx per message is cheap but a cached ctx per
+ * (k, n) is what INTEGRATION.md recommends. */
+int rs_new(int k, int n, rs_ctx **out);                 /* current HIP device */
+int rs_new_on_device(int k, int n, int device, rs_ctx **out);
+void rs_free(rs_ctx *ctx);
+int rs_k(const rs_ctx *ctx);
+int rs_n(const rs_ctx *ctx);
+int rs_device(const rs_ctx *ctx);
+/* Copy of the n x k row-major encode matrix (infectious FEC.enc_matrix). */
+int rs_encode_matrix(const rs_ctx *ctx, uint8_t *out);
+const char *rs_strerror(int status);
+
+/* ---- host-buffer API (the cgo path) -------------------------------------
+ * rs_encode replaces (*FEC).Encode(input, output) at main.go:262.
+ * input: len bytes, len % k == 0 (else RS_ELEN_NOT_MULTIPLE), S = len / k.
+ * Data shares 0..k-1 are views input[i*S, (i+1)*S) (systematic, exactly as
+ * infectious emits them); parity shares k..n-1 are written to
+ * parity[(i-k)*S, (i-k+1)*S).  len == 0 is allowed (empty shares). */
+int rs_encode(rs_ctx *ctx, const uint8_t *input, size_t len, uint8_t *parity);
+
+/* rs_decode replaces (*FEC).Decode(dst, shares) at main.go:77 (the Correct
+ * step is a no-op for exactly k distinct shares, the only case the plugin
+ * produces: main.go:65).  numbers[count] / shares[count] describe the
+ * received infectious.Share values; both arrays are sorted in place by
+ * number, like infectious sorts the caller's slice.  Each share holds
+ * share_len bytes.  dst receives k * share_len bytes = the original input.
+ * Errors: count < k -> RS_ENOT_ENOUGH; number outside [0, n) ->
+ * RS_EBAD_SHARE_ID; fewer than k distinct numbers -> RS_ESINGULAR. */
+int rs_decode(rs_ctx *ctx, int *numbers, const uint8_t **shares, int count,
+              size_t share_len, uint8_t *dst);
+
+/* ---- device-resident batched API (many stripes per launch) ---------------
+ * Stripe s, shard i lives at
+ *     i <  k:  data   + s * data_stripe_stride   + i       * shard_pitch
+ *     i >= k:  parity + s * parity_stripe_stride + (i - k) * shard_pitch
+ * shard_len bytes are coded per shard; shard_pitch, both stripe strides and
+ * both base pointers must be multiples of 16 and shard_pitch >=
+ * round_up(shard_len, 16) (bytes between shard_len and the next multiple of
+ * 16 are coded too: padding, never read back by the host API).
+ *
+ * rs_encode_stripes: parity of every stripe (stripe-batched (*FEC).Encode).
+ * Enqueued on stream; returns when the launch is queued. */
+int rs_encode_stripes(rs_ctx *ctx, const void *data, size_t data_stripe_stride,
+                      void *parity, size_t parity_stripe_stride, size_t shard_pitch,
+                      size_t shard_len, size_t stripes, void *stream);
+
+/* rs_reconstruct_stripes: erased is a HOST array of stripes * n flags
+ * (non-zero = shard i of stripe s is missing).  Every erased shard, data or
+ * parity, is regenerated in place from k survivors chosen like infectious
+ * Rebuild (data shares first, then the highest-numbered parity).  Per-pattern
+ * decode matrices are inverted once and cached in the ctx.  A stripe with
+ * more than m erasures -> RS_ENOT_ENOUGH (nothing is launched).  Enqueued on
+ * stream (the small pattern tables are staged through pinned memory). */
+int rs_reconstruct_stripes(rs_ctx *ctx, void *data, size_t data_stripe_stride,
+                           void *parity, size_t parity_stripe_stride, size_t shard_pitch,
+                           size_t shard_len, size_t stripes, const uint8_t *erased,
+                           void *stream);
+
+/* Cached decode patterns held by the ctx (diagnostics / tests). */
+int rs_pattern_count(const rs_ctx *ctx);
+
+/* Precompute (invert and upload) the decode patterns of every erasure set of
+ * 1..max_erasures shards (max_erasures <= m), e.g. the 1,470 patterns of
+ * RS(10,4) with <= 4 erasures, so later rs_reconstruct_stripes calls only
+ * index them.  RS_EINVAL if that would exceed 2^20 patterns. */
+int rs_prepare_patterns(rs_ctx *ctx, int max_erasures, void *stream);
+
+/* ---- memory helpers ------------------------------------------------------ */
+void *rs_pinned_alloc(size_t bytes); /* hipHostMalloc; NULL on failure */
+void rs_pinned_free(void *p);
+int rs_device_alloc(rs_ctx *ctx, size_t bytes, void **out);
+int rs_device_free(rs_ctx *ctx, void *p);
+int rs_stream_sync(rs_ctx *ctx, void *stream);
+
+/* ---- bench / test utility (not on the codec path) ------------------------
+ * Fill len bytes of device memory with the splitmix64 byte stream of seed
+ * (byte i = byte i%8 of splitmix64(seed + (i/8 + 1) * golden)), the same
+ * stream the CPU baseline generates. */
+int rs_fill_splitmix(rs_ctx *ctx, void *dev, size_t len, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSMI_H */

@@ -1,0 +1,145 @@
+// gf256.cpp -- see gf256.hpp.
+#include "gf256.hpp"
+
+#include <cstring>
+
+namespace rsmi {
+
+Field::Field() {
+    // exp[i] = 2^i by repeated doubling modulo the polynomial.
+    uint32_t x = 1;
+    for (int i = 0; i < 255; ++i) {
+        exp[i] = static_cast<uint8_t>(x);
+        exp[i + 255] = static_cast<uint8_t>(x);
+        log[x] = static_cast<uint8_t>(i);
+        x <<= 1;
+        if (x & 0x100) x ^= kPoly;
+    }
+    exp[510] = exp[0];
+    exp[511] = exp[1];
+    log[0] = 0;  // unused: 0 has no logarithm
+    inv[0] = 0;
+    for (int a = 1; a < 256; ++a) inv[a] = exp[255 - log[a]];
+    for (int a = 0; a < 256; ++a)
+        for (int b = 0; b < 256; ++b)
+            mul[a][b] = (a && b) ? exp[log[a] + log[b]] : 0;
+}
+
+const Field& field() {
+    static const Field f;
+    return f;
+}
+
+uint8_t eval_point(int r) { return r == 0 ? 0 : field().exp[r % 255]; }
+
+static uint8_t gpow(uint8_t x, int e) {
+    if (e == 0) return 1;
+    if (x == 0) return 0;
+    const Field& f = field();
+    return f.exp[(f.log[x] * e) % 255];
+}
+
+bool invert(uint8_t* a, int k) {
+    // Gauss-Jordan on [A | I] with row pivoting.
+    const Field& f = field();
+    std::vector<uint8_t> aug(static_cast<size_t>(k) * 2 * k, 0);
+    const int w = 2 * k;
+    for (int r = 0; r < k; ++r) {
+        std::memcpy(&aug[r * w], a + r * k, k);
+        aug[r * w + k + r] = 1;
+    }
+    for (int col = 0; col < k; ++col) {
+        int piv = -1;
+        for (int r = col; r < k; ++r)
+            if (aug[r * w + col]) { piv = r; break; }
+        if (piv < 0) return false;
+        if (piv != col)
+            for (int c = 0; c < w; ++c) std::swap(aug[piv * w + c], aug[col * w + c]);
+        const uint8_t s = f.inv[aug[col * w + col]];
+        for (int c = 0; c < w; ++c) aug[col * w + c] = f.mul[s][aug[col * w + c]];
+        for (int r = 0; r < k; ++r) {
+            if (r == col) continue;
+            const uint8_t fac = aug[r * w + col];
+            if (!fac) continue;
+            for (int c = 0; c < w; ++c) aug[r * w + c] ^= f.mul[fac][aug[col * w + c]];
+        }
+    }
+    for (int r = 0; r < k; ++r) std::memcpy(a + r * k, &aug[r * w + k], k);
+    return true;
+}
+
+std::vector<uint8_t> systematic_matrix(int k, int n) {
+    const Field& f = field();
+    std::vector<uint8_t> V(static_cast<size_t>(n) * k);
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < k; ++c) V[r * k + c] = gpow(eval_point(r), c);
+    std::vector<uint8_t> top(V.begin(), V.begin() + static_cast<size_t>(k) * k);
+    invert(top.data(), k);  // Vandermonde with distinct points: never singular
+    std::vector<uint8_t> E(static_cast<size_t>(n) * k, 0);
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < k; ++c) {
+            uint8_t acc = 0;
+            for (int i = 0; i < k; ++i) acc ^= f.mul[V[r * k + i]][top[i * k + c]];
+            E[r * k + c] = acc;
+        }
+    // The top block is exactly the identity by construction; pin it.
+    for (int r = 0; r < k; ++r)
+        for (int c = 0; c < k; ++c) E[r * k + c] = (r == c);
+    return E;
+}
+
+std::vector<int> choose_survivors(const uint8_t* present, int k, int n) {
+    std::vector<int> out;
+    int avail = 0;
+    for (int i = 0; i < n; ++i) avail += present[i] ? 1 : 0;
+    if (avail < k) return out;
+    std::vector<uint8_t> used(n, 0);
+    int hi = n - 1;
+    for (int i = 0; i < k; ++i) {
+        if (present[i] && !used[i]) {
+            out.push_back(i);
+            used[i] = 1;
+            continue;
+        }
+        while (hi >= 0 && (!present[hi] || used[hi])) --hi;
+        out.push_back(hi);
+        used[hi] = 1;
+    }
+    return out;
+}
+
+bool decode_rows(const std::vector<uint8_t>& enc, int k, int n, const std::vector<int>& surv,
+                 const std::vector<int>& targets, std::vector<uint8_t>& rows) {
+    (void)n;
+    const Field& f = field();
+    std::vector<uint8_t> M(static_cast<size_t>(k) * k);
+    for (int i = 0; i < k; ++i) std::memcpy(&M[i * k], &enc[static_cast<size_t>(surv[i]) * k], k);
+    if (!invert(M.data(), k)) return false;
+    // shard[t] = enc[t] . data = enc[t] . (M^-1 . survivors)
+    rows.assign(targets.size() * static_cast<size_t>(k), 0);
+    for (size_t t = 0; t < targets.size(); ++t) {
+        const uint8_t* e = &enc[static_cast<size_t>(targets[t]) * k];
+        for (int c = 0; c < k; ++c) {
+            uint8_t acc = 0;
+            for (int i = 0; i < k; ++i) acc ^= f.mul[e[i]][M[i * k + c]];
+            rows[t * k + c] = acc;
+        }
+    }
+    return true;
+}
+
+void coef_tables(uint8_t c, uint32_t w[5]) {
+    const Field& f = field();
+    auto pack = [&](int base, int step, int count) {
+        uint32_t v = 0;
+        for (int i = 0; i < count; ++i) v |= uint32_t(f.mul[c][(base + i * step) & 0xff]) << (8 * i);
+        return v;
+    };
+    w[0] = pack(0, 1, 4);
+    w[1] = pack(4, 1, 4);
+    w[2] = pack(0, 8, 4);
+    w[3] = pack(32, 8, 4);
+    w[4] = pack(0, 64, 4);
+}
+
+}  // namespace rsmi

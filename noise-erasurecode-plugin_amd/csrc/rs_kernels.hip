@@ -1,0 +1,310 @@
+// rs_kernels.hip -- CDNA4 (gfx950) kernels for GF(2^8) coding-matrix x
+// shard-stripe products: the parity loop of infectious (*FEC).Encode
+// (reference call site main.go:262) and the inverted-submatrix loop of
+// (*FEC).Rebuild (reference call site main.go:77), batched over stripes.
+//
+// Arithmetic (no MFMA: GF(2^8) is not an FP contraction):
+//   c * x for a byte x is split over the bit fields x[2:0], x[5:3], x[7:6]:
+//       c*x = Ta[x & 7] ^ Tb[(x >> 3) & 7] ^ Tc[x >> 6]
+//   Ta/Tb are 8-entry byte tables (two dwords each), Tc a 4-entry table (one
+//   dword); each lookup is one v_perm_b32 on four packed bytes at once.
+//   The five table dwords per coefficient are built per block from the raw
+//   coefficient bytes and staged in LDS; a lane reads a coefficient's tables
+//   with broadcast ds_read_b128 and XOR-accumulates in VGPRs (v_bitop3_b32).
+// Memory: each lane owns one 16-byte column of every survivor shard
+// (global_load_dwordx4, fully coalesced: 64 lanes = 1 KiB contiguous per
+// shard); outputs are written once with global_store_dwordx4.
+#include "rs_kernels.hpp"
+
+#include <algorithm>
+
+namespace rsmi {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t xtime(uint32_t a) {
+    a <<= 1;
+    return a ^ ((a & 0x100u) ? 0x11Du : 0u);
+}
+
+// Split-table words of coefficient c (host twin: gf256.cpp coef_tables).
+__device__ void build_tables(uint32_t c, uint32_t* w) {
+    uint32_t p[8];
+    p[0] = c;
+#pragma unroll
+    for (int b = 1; b < 8; ++b) p[b] = xtime(p[b - 1]);
+    auto val = [&](uint32_t v) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) r ^= ((v >> b) & 1u) ? p[b] : 0u;
+        return r;
+    };
+    auto pack = [&](uint32_t base, uint32_t step) {
+        return val(base) | (val(base + step) << 8) | (val(base + 2 * step) << 16) |
+               (val(base + 3 * step) << 24);
+    };
+    w[0] = pack(0, 1);
+    w[1] = pack(4, 1);
+    w[2] = pack(0, 8);
+    w[3] = pack(32, 8);
+    w[4] = pack(0, 64) & 0xFFFFFFFFu;
+}
+
+// acc ^= c * x on four packed bytes, c given by its table words T[0..4];
+// ia/ib/ic are the per-byte bit-field selectors of x.
+__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, const uint32_t* T, uint32_t ia,
+                                           uint32_t ib, uint32_t ic) {
+    const uint32_t la = __builtin_amdgcn_perm(T[1], T[0], ia);
+    const uint32_t lb = __builtin_amdgcn_perm(T[3], T[2], ib);
+    const uint32_t lc = __builtin_amdgcn_perm(T[4], T[4], ic);
+    return xor3(acc, la, lb) ^ lc;
+}
+
+// Compiler fence for memory operations: keeps LDS table reads where they are
+// written (LICM would otherwise hoist all k*MG*5 table dwords into VGPRs).
+#define RS_MEM_FENCE() asm volatile("" ::: "memory")
+
+constexpr int kRowsPerStep = 4;               // output rows per table sub-step
+constexpr int kStepWords = kRowsPerStep * 5;  // table dwords per sub-step (5 x b128)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 GlobalCU4;
+typedef __attribute__((address_space(1))) u32x4 GlobalU4;
+
+// Global (not flat) 16-byte load/store: flat ops would count on lgkmcnt too
+// and serialise against the LDS table reads.
+__device__ __forceinline__ uint4 gload16(const uint8_t* p) {
+    const u32x4 v = *(GlobalCU4*)(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    *(GlobalU4*)(p) = w;
+}
+
+// Wave-uniform 64-bit value into SGPRs.
+__device__ __forceinline__ uint8_t* uniform_ptr(uint8_t* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+    return reinterpret_cast<uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ void load_step(const uint4* src, uint32_t (&T)[kStepWords]) {
+#pragma unroll
+    for (int w = 0; w < kStepWords / 4; ++w) {
+        const uint4 v = src[w];
+        T[4 * w + 0] = v.x;
+        T[4 * w + 1] = v.y;
+        T[4 * w + 2] = v.z;
+        T[4 * w + 3] = v.w;
+    }
+}
+
+// acc[r][w] ^= coef(row r) * x.w for the four rows of one sub-step.
+__device__ __forceinline__ void mac_step(uint32_t (&acc)[kRowsPerStep][4], const uint4& x,
+                                         const uint32_t (&T)[kStepWords]) {
+    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t ia = xw[w] & 0x07070707u;
+        const uint32_t ib = (xw[w] >> 3) & 0x07070707u;
+        const uint32_t ic = (xw[w] >> 6) & 0x03030303u;
+#pragma unroll
+        for (int r = 0; r < kRowsPerStep; ++r) acc[r][w] = gf_mac(acc[r][w], &T[r * 5], ia, ib, ic);
+    }
+}
+
+// Step boundary: the accumulators of the finished sub-step are inputs of the
+// asm, so its arithmetic completes before the boundary, and the memory
+// clobber keeps the next sub-step's LDS reads after it.  At most two
+// sub-steps of tables (2 x 20 dwords) are live at any time.
+__device__ __forceinline__ void step_fence(uint32_t (&acc)[kRowsPerStep][4]) {
+#pragma unroll
+    for (int r = 0; r < kRowsPerStep; ++r)
+        asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3])::"memory");
+}
+
+// One block codes a chunk of 16-byte columns of one stripe for one group of
+// MG output rows.  LDS: [k][MG/4][20] table dwords | k survivor pointers.
+template <int K, int MG>
+__global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
+    static_assert(MG % kRowsPerStep == 0, "MG must be a multiple of 4");
+    constexpr int TG = MG / kRowsPerStep;                 // sub-steps per survivor
+    constexpr bool kRegPtrs = K > 0 && K <= 16;           // survivor bases kept in SGPRs
+    constexpr int JB = (K == 0) ? 8 : (K <= 16 ? K : 8);  // survivor loads in flight
+    const int k = K ? K : static_cast<int>(a.k);
+    extern __shared__ uint4 lds4[];
+    uint32_t* tw = reinterpret_cast<uint32_t*>(lds4);
+    uint8_t** sptr = reinterpret_cast<uint8_t**>(tw + k * MG * 5);
+
+    uint64_t b = blockIdx.x;
+    const uint32_t grp = static_cast<uint32_t>(b % a.groups);
+    b /= a.groups;
+    const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);
+    const uint64_t s = b / a.chunks;
+    const uint32_t pat = __builtin_amdgcn_readfirstlane(a.stripe_pat ? a.stripe_pat[s] : 0u);
+    const int e = static_cast<int>(__builtin_amdgcn_readfirstlane(a.cnt[pat]));
+    const int row0 = static_cast<int>(grp) * MG;
+    if (row0 >= e) return;  // whole block: uniform
+    const int eg = min(MG, e - row0);
+
+    auto shard = [&](uint32_t id) -> uint8_t* {
+        return id < a.k ? a.data + s * a.data_ss + static_cast<uint64_t>(id) * a.pitch
+                        : a.parity + s * a.parity_ss + static_cast<uint64_t>(id - a.k) * a.pitch;
+    };
+    const uint32_t* srcid = a.src + static_cast<size_t>(pat) * k;
+    const uint32_t* dstid = a.dst + static_cast<size_t>(pat) * a.m + row0;
+    uint8_t* sp[kRegPtrs ? K : 1];
+    if constexpr (kRegPtrs) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) sp[j] = uniform_ptr(shard(__builtin_amdgcn_readfirstlane(srcid[j])));
+    } else {
+        for (int i = threadIdx.x; i < k; i += kBlock) sptr[i] = shard(srcid[i]);
+    }
+    uint8_t* dp[MG];
+#pragma unroll
+    for (int t = 0; t < MG; ++t)
+        dp[t] = t < eg ? uniform_ptr(shard(__builtin_amdgcn_readfirstlane(dstid[t]))) : nullptr;
+    // Split tables of rows [row0, row0 + MG): sub-step (j, g) holds rows
+    // 4g..4g+3 as 4 x 5 dwords.
+    const uint8_t* coef = a.coef + (static_cast<size_t>(pat) * a.m + row0) * k;
+    for (int idx = threadIdx.x; idx < k * MG; idx += kBlock) {
+        const int j = idx / MG, t = idx - j * MG;
+        const uint32_t c = (t < eg) ? coef[t * k + j] : 0u;
+        build_tables(c, &tw[(j * TG + t / kRowsPerStep) * kStepWords + (t % kRowsPerStep) * 5]);
+    }
+    __syncthreads();
+
+    const uint32_t last = a.ncols16 - 1;
+    for (uint32_t it = 0; it < a.iters; ++it) {
+        const uint32_t colbase = (chunk * a.iters + it) * kBlock;
+        if (colbase >= a.ncols16) break;
+        RS_MEM_FENCE();
+        const uint32_t col = colbase + threadIdx.x;
+        const bool ok = col <= last;
+        // Tail lanes re-read the last column (always in bounds) and skip the store.
+        const uint32_t off = (ok ? col : last) * 16u;
+        uint32_t acc[TG][kRowsPerStep][4];
+#pragma unroll
+        for (int g = 0; g < TG; ++g)
+#pragma unroll
+            for (int r = 0; r < kRowsPerStep; ++r)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc[g][r][w] = 0u;
+
+        for (int jb = 0; jb < k; jb += JB) {
+            uint4 x[JB];
+#pragma unroll
+            for (int q = 0; q < JB; ++q) {
+                if (K == 0 && jb + q >= k) break;
+                const uint8_t* base = kRegPtrs ? sp[kRegPtrs ? jb + q : 0] : uniform_ptr(sptr[jb + q]);
+                x[q] = gload16(base + off);
+            }
+            uint32_t TA[kStepWords], TB[kStepWords];
+            load_step(lds4 + static_cast<size_t>(jb * TG) * (kStepWords / 4), TA);
+#pragma unroll
+            for (int q = 0; q < JB; ++q) {
+                if (K == 0 && jb + q >= k) break;
+#pragma unroll
+                for (int g = 0; g < TG; ++g) {
+                    // Sub-step (jb+q, g): prefetch the next one's tables, then
+                    // multiply with the current ones (TA/TB alternate; the
+                    // unrolled loop turns the copy into register renaming).
+                    const int step = (jb + q) * TG + g;
+                    const bool more = (g + 1 < TG) || (q + 1 < JB && (K != 0 || jb + q + 1 < k));
+                    if (more) load_step(lds4 + static_cast<size_t>(step + 1) * (kStepWords / 4), TB);
+                    mac_step(acc[g], x[q], TA);
+                    step_fence(acc[g]);
+#pragma unroll
+                    for (int w = 0; w < kStepWords; ++w) TA[w] = TB[w];
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < TG; ++g)
+#pragma unroll
+            for (int r = 0; r < kRowsPerStep; ++r) {
+                const int t = g * kRowsPerStep + r;
+                if (t >= eg) break;
+                if (ok) gstore16(dp[t] + off, make_uint4(acc[g][r][0], acc[g][r][1], acc[g][r][2], acc[g][r][3]));
+            }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint8_t* p, size_t len,
+                                                               uint64_t seed) {
+    const size_t nq = len / 8;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t q = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; q <= nq; q += stride) {
+        uint64_t z = seed + (q + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        if (q < nq) {
+            reinterpret_cast<uint64_t*>(p)[q] = z;
+        } else {
+            for (size_t i = nq * 8; i < len; ++i) p[i] = static_cast<uint8_t>(z >> (8 * (i - nq * 8)));
+        }
+    }
+}
+
+struct Variant {
+    int K, MG;
+    const char* name;
+    void (*fn)(MatArgs);
+};
+
+#define RS_VARIANT(K, MG) {K, MG, "K" #K "_MG" #MG, rs_matmul_kernel<K, MG>}
+// Specialised variants for the configurations the plugin and BASELINE use,
+// then runtime-k fall-backs (k up to 256).
+const Variant kVariants[] = {
+    RS_VARIANT(10, 4),   // RS(10,4): BASELINE configs 1-4
+    RS_VARIANT(4, 4),    // RS(4,2): plugin default (main.go:34-35)
+    RS_VARIANT(8, 8),    // infectious example RS(8,14)
+    RS_VARIANT(64, 16),  // RS(64,16): BASELINE config 5
+    RS_VARIANT(0, 4),
+    RS_VARIANT(0, 8),
+};
+#undef RS_VARIANT
+
+const Variant& pick(int k, int m) {
+    for (const Variant& v : kVariants)
+        if (v.K != 0 && v.K == k && m <= v.MG) return v;
+    if (k == 64) return kVariants[3];  // RS(64, m > 16): row groups of 16
+    return m <= 4 ? kVariants[4] : kVariants[5];
+}
+
+}  // namespace
+
+const char* variant_name(int k, int m) { return pick(k, m).name; }
+
+hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
+    if (a.stripes == 0 || a.ncols16 == 0 || max_e <= 0) return hipSuccess;
+    const Variant& v = pick(static_cast<int>(a.k), static_cast<int>(a.m));
+    const uint32_t total_it = (a.ncols16 + kBlock - 1) / kBlock;
+    a.iters = std::min<uint32_t>(16u, total_it);
+    a.chunks = (total_it + a.iters - 1) / a.iters;
+    a.groups = static_cast<uint32_t>((max_e + v.MG - 1) / v.MG);
+    const size_t lds = static_cast<size_t>(a.k) * v.MG * 5 * 4 + a.k * sizeof(void*);
+    const uint64_t blocks = a.stripes * a.chunks * a.groups;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+    hipLaunchKernelGGL(v.fn, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix(void* dev, size_t len, uint64_t seed, hipStream_t stream) {
+    if (len == 0) return hipSuccess;
+    const size_t nq = len / 8 + 1;
+    const size_t blocks = std::min<size_t>((nq + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+                       stream, static_cast<uint8_t*>(dev), len, seed);
+    return hipGetLastError();
+}
+
+}  // namespace rsmi

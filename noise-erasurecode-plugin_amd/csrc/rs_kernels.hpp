@@ -1,0 +1,45 @@
+// rs_kernels.hpp -- launch interface of the GF(2^8) matrix x stripe kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rsmi {
+
+// One launch codes many stripes.  For stripe s the kernel reads the k
+// survivor shards src[pat][0..k-1] and writes the e = cnt[pat] output shards
+// dst[pat][0..e-1]:  out_t = sum_c coef[pat][t][c] * shard[src[pat][c]].
+// Encode is the single pattern {src = 0..k-1, dst = k..n-1, coef = E_bottom}.
+// Shard id i < k lives in the data region, i >= k in the parity region
+// (see rsmi.h, rs_encode_stripes).
+struct MatArgs {
+    uint8_t* data;
+    uint8_t* parity;
+    uint64_t data_ss;    // data stripe stride (bytes)
+    uint64_t parity_ss;  // parity stripe stride (bytes)
+    uint64_t pitch;      // shard pitch (bytes)
+    uint64_t stripes;
+    uint32_t ncols16;    // 16-byte columns per shard = ceil(shard_len / 16)
+    uint32_t chunks;     // column chunks per stripe
+    uint32_t groups;     // output-row groups per stripe
+    uint32_t iters;      // block iterations per chunk
+    uint32_t k, m;
+    const uint8_t* coef;         // [npat][m][k]
+    const uint32_t* src;         // [npat][k]   survivor shard ids
+    const uint32_t* dst;         // [npat][m]   output shard ids
+    const uint32_t* cnt;         // [npat]      outputs per pattern (<= m)
+    const uint32_t* stripe_pat;  // [stripes] pattern id, or nullptr: pattern 0
+};
+
+// Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel
+// variant for (k, m).  max_e bounds cnt[] over all patterns.
+hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream);
+
+// Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
+const char* variant_name(int k, int m);
+
+// splitmix64 byte stream fill (bench/test utility).
+hipError_t launch_fill_splitmix(void* dev, size_t len, uint64_t seed, hipStream_t stream);
+
+}  // namespace rsmi

@@ -1,0 +1,565 @@
+// rsmi.cpp -- C ABI of the engine (include/rsmi.h).  Host-side bookkeeping
+// around the HIP kernels: encode/decode matrices, the per-ctx decode-pattern
+// cache, device workspaces and pinned staging.  The GF products themselves
+// always run on the GPU; there is no CPU compute fallback.
+#include "../../include/rsmi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gf256.hpp"
+#include "rs_kernels.hpp"
+
+namespace {
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Restores the caller's current HIP device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// A growable device buffer.  Growing synchronises the device first, since
+// earlier launches may still read the old allocation.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool reserve(size_t bytes) {
+        if (bytes <= cap) return true;
+        if (p) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = std::max({bytes, size_t(4096), 2 * cap});
+        if (hipMalloc(&p, want) != hipSuccess) return false;
+        cap = want;
+        return true;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// Pinned host staging whose reuse waits for the copies that read it.
+struct Staging {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    bool acquire(size_t bytes) {
+        if (pending) {
+            (void)hipEventSynchronize(done);
+            pending = false;
+        }
+        if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) return false;
+        if (bytes <= cap) return true;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(bytes, size_t(1) << 16);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return false;
+        cap = want;
+        return true;
+    }
+    void release_after(hipStream_t s) {
+        if (hipEventRecord(done, s) == hipSuccess) pending = true;
+    }
+    void destroy() {
+        if (pending) (void)hipEventSynchronize(done);
+        if (p) (void)hipHostFree(p);
+        if (done) (void)hipEventDestroy(done);
+        p = nullptr;
+        done = nullptr;
+    }
+};
+
+}  // namespace
+
+struct rs_ctx {
+    int k = 0, n = 0, m = 0, device = 0;
+    std::vector<uint8_t> enc;  // n x k systematic matrix
+    std::mutex mu;
+    hipStream_t stream = nullptr;  // used by the host-buffer API
+
+    // Encode pattern on the device (PatBlob layout, one pattern).
+    DevBuf d_encpat;
+
+    // Decode-pattern cache (host mirror + device copy of every pattern).
+    std::unordered_map<std::string, int> pat_index;
+    std::vector<uint8_t> h_coef;
+    std::vector<uint32_t> h_src, h_dst, h_cnt;
+    DevBuf d_pats;
+    size_t uploaded = 0;  // patterns present on the device
+    DevBuf d_stripe_pat;
+    Staging st_pat;      // pattern-table uploads
+    Staging st_stripe;   // stripe->pattern ids
+
+    // Host-buffer API workspaces.
+    DevBuf d_work;
+    DevBuf d_onepat;
+    Staging st_one;
+};
+
+namespace {
+
+int hip_status(hipError_t e) { return e == hipSuccess ? RS_OK : RS_EDEVICE; }
+
+// Device blob of npat patterns: coef bytes [npat][m][k] (padded to 16) |
+// src u32 [npat][k] | dst u32 [npat][m] | cnt u32 [npat].
+struct PatLayout {
+    size_t coef, src, dst, cnt, total;
+    PatLayout(const rs_ctx* c, size_t npat) {
+        coef = 0;
+        src = round_up(npat * c->m * c->k, 16);
+        dst = src + npat * c->k * 4;
+        cnt = dst + npat * c->m * 4;
+        total = cnt + npat * 4;
+    }
+};
+
+void pack_patterns(const rs_ctx* c, size_t npat, const uint8_t* coef, const uint32_t* src,
+                   const uint32_t* dst, const uint32_t* cnt, uint8_t* out) {
+    PatLayout L(c, npat);
+    std::memset(out, 0, L.total);
+    std::memcpy(out + L.coef, coef, npat * c->m * c->k);
+    std::memcpy(out + L.src, src, npat * c->k * 4);
+    std::memcpy(out + L.dst, dst, npat * c->m * 4);
+    std::memcpy(out + L.cnt, cnt, npat * 4);
+}
+
+void set_patterns(const rs_ctx* c, size_t npat, const void* dev, rsmi::MatArgs& a) {
+    PatLayout L(c, npat);
+    const uint8_t* b = static_cast<const uint8_t*>(dev);
+    a.coef = b + L.coef;
+    a.src = reinterpret_cast<const uint32_t*>(b + L.src);
+    a.dst = reinterpret_cast<const uint32_t*>(b + L.dst);
+    a.cnt = reinterpret_cast<const uint32_t*>(b + L.cnt);
+}
+
+bool check_stripes_args(const rs_ctx* c, const void* data, size_t dss, const void* parity,
+                        size_t pss, size_t pitch, size_t len) {
+    auto al = [](uintptr_t v) { return (v & 15u) == 0; };
+    if (!data || (!parity && c->m > 0)) return false;
+    if (!al(reinterpret_cast<uintptr_t>(data)) || !al(reinterpret_cast<uintptr_t>(parity)))
+        return false;
+    if (!al(dss) || !al(pss) || !al(pitch)) return false;
+    if (pitch < round_up(len, 16)) return false;
+    if (round_up(len, 16) / 16 >= (size_t(1) << 28)) return false;  // 32-bit column offsets
+    return true;
+}
+
+rsmi::MatArgs base_args(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
+                        size_t pitch, size_t len, size_t stripes) {
+    rsmi::MatArgs a{};
+    a.data = static_cast<uint8_t*>(data);
+    a.parity = static_cast<uint8_t*>(parity);
+    a.data_ss = dss;
+    a.parity_ss = pss;
+    a.pitch = pitch;
+    a.stripes = stripes;
+    a.ncols16 = static_cast<uint32_t>(round_up(len, 16) / 16);
+    a.k = static_cast<uint32_t>(c->k);
+    a.m = static_cast<uint32_t>(c->m);
+    return a;
+}
+
+// Finds or creates the decode pattern for `erased` (n flags); -1 on error
+// with *err set.
+int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
+    std::string key(reinterpret_cast<const char*>(erased), static_cast<size_t>(c->n));
+    for (char& ch : key) ch = ch ? 1 : 0;
+    auto it = c->pat_index.find(key);
+    if (it != c->pat_index.end()) return it->second;
+    std::vector<uint8_t> present(c->n);
+    std::vector<int> targets;
+    for (int i = 0; i < c->n; ++i) {
+        present[i] = key[i] ? 0 : 1;
+        if (key[i]) targets.push_back(i);
+    }
+    if (static_cast<int>(targets.size()) > c->m) {
+        *err = RS_ENOT_ENOUGH;
+        return -1;
+    }
+    if (c->pat_index.size() >= (size_t(1) << 20)) {  // bound the cache: start over
+        (void)hipDeviceSynchronize();
+        c->pat_index.clear();
+        c->h_coef.clear();
+        c->h_src.clear();
+        c->h_dst.clear();
+        c->h_cnt.clear();
+        c->uploaded = 0;
+    }
+    std::vector<int> surv = rsmi::choose_survivors(present.data(), c->k, c->n);
+    std::vector<uint8_t> rows;
+    if (!targets.empty() && !rsmi::decode_rows(c->enc, c->k, c->n, surv, targets, rows)) {
+        *err = RS_ESINGULAR;
+        return -1;
+    }
+    const int id = static_cast<int>(c->pat_index.size());
+    const size_t mk = static_cast<size_t>(c->m) * c->k;
+    c->h_coef.resize((id + 1) * mk, 0);
+    std::copy(rows.begin(), rows.end(), c->h_coef.begin() + id * mk);
+    for (int v : surv) c->h_src.push_back(static_cast<uint32_t>(v));
+    for (int t = 0; t < c->m; ++t)
+        c->h_dst.push_back(t < static_cast<int>(targets.size()) ? static_cast<uint32_t>(targets[t]) : 0u);
+    c->h_cnt.push_back(static_cast<uint32_t>(targets.size()));
+    c->pat_index.emplace(std::move(key), id);
+    return id;
+}
+
+int upload_patterns(rs_ctx* c, hipStream_t s) {
+    const size_t npat = c->h_cnt.size();
+    if (npat == c->uploaded) return RS_OK;
+    PatLayout L(c, npat);
+    if (!c->d_pats.reserve(L.total)) return RS_ENOMEM;
+    if (!c->st_pat.acquire(L.total)) return RS_ENOMEM;
+    uint8_t* h = static_cast<uint8_t*>(c->st_pat.p);
+    pack_patterns(c, npat, c->h_coef.data(), c->h_src.data(), c->h_dst.data(), c->h_cnt.data(), h);
+    hipError_t e = hipMemcpyAsync(c->d_pats.p, h, L.total, hipMemcpyHostToDevice, s);
+    c->st_pat.release_after(s);
+    if (e != hipSuccess) return RS_EDEVICE;
+    c->uploaded = npat;
+    return RS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rs_strerror(int st) {
+    switch (st) {
+        case RS_OK: return "ok";
+        case RS_EINVAL_KN: return "requires 1 <= k <= n <= 256";
+        case RS_ELEN_NOT_MULTIPLE: return "input length must be a multiple of k";
+        case RS_ENOT_ENOUGH: return "not enough shares";
+        case RS_EBAD_SHARE_ID: return "invalid share id";
+        case RS_ESINGULAR: return "singular matrix";
+        case RS_ENO_SHARES: return "must specify at least one share";
+        case RS_ESHARE_LEN: return "shares have different lengths";
+        case RS_EINVAL: return "invalid argument";
+        case RS_EDEVICE: return "HIP device error";
+        case RS_ENOMEM: return "out of memory";
+        default: return "unknown error";
+    }
+}
+
+int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
+    if (!out) return RS_EINVAL;
+    *out = nullptr;
+    if (k <= 0 || n <= 0 || k > 256 || n > 256 || k > n) return RS_EINVAL_KN;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+        return RS_EDEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RS_EDEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RS_EDEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return RS_EDEVICE;
+    rs_ctx* c = new (std::nothrow) rs_ctx;
+    if (!c) return RS_ENOMEM;
+    c->k = k;
+    c->n = n;
+    c->m = n - k;
+    c->device = device;
+    c->enc = rsmi::systematic_matrix(k, n);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return RS_EDEVICE;
+    }
+    // Encode pattern: coef = bottom rows, src = 0..k-1, dst = k..n-1, cnt = m.
+    std::vector<uint32_t> src(k), dst(c->m), cnt(1, static_cast<uint32_t>(c->m));
+    for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
+    for (int t = 0; t < c->m; ++t) dst[t] = static_cast<uint32_t>(k + t);
+    std::vector<uint8_t> pat(PatLayout(c, 1).total);
+    pack_patterns(c, 1, c->enc.data() + static_cast<size_t>(k) * k, src.data(), dst.data(),
+                  cnt.data(), pat.data());
+    if (!c->d_encpat.reserve(pat.size()) ||
+        hipMemcpy(c->d_encpat.p, pat.data(), pat.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        rs_free(c);
+        return RS_EDEVICE;
+    }
+    *out = c;
+    return RS_OK;
+}
+
+int rs_new(int k, int n, rs_ctx** out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return rs_new_on_device(k, n, dev, out);
+}
+
+void rs_free(rs_ctx* c) {
+    if (!c) return;
+    {
+        DeviceGuard g(c->device);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        (void)hipDeviceSynchronize();
+        c->st_pat.destroy();
+        c->st_stripe.destroy();
+        c->st_one.destroy();
+        for (DevBuf* b : {&c->d_encpat, &c->d_pats, &c->d_stripe_pat, &c->d_work, &c->d_onepat})
+            b->release();
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+int rs_k(const rs_ctx* c) { return c ? c->k : RS_EINVAL; }
+int rs_n(const rs_ctx* c) { return c ? c->n : RS_EINVAL; }
+int rs_device(const rs_ctx* c) { return c ? c->device : RS_EINVAL; }
+
+int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
+    if (!c || !out) return RS_EINVAL;
+    std::memcpy(out, c->enc.data(), c->enc.size());
+    return RS_OK;
+}
+
+int rs_pattern_count(const rs_ctx* c) {
+    return c ? static_cast<int>(c->pat_index.size()) : RS_EINVAL;
+}
+
+int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
+    if (!c || max_e < 0 || max_e > c->m) return RS_EINVAL;
+    // count = sum_{e=1..max_e} C(n, e)
+    double total = 0, binom = 1;
+    for (int e = 1; e <= max_e; ++e) {
+        binom = binom * (c->n - e + 1) / e;
+        total += binom;
+    }
+    if (total > double(1 << 20)) return RS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    std::vector<uint8_t> er(c->n);
+    std::vector<int> idx;
+    for (int e = 1; e <= max_e; ++e) {
+        idx.resize(e);
+        for (int i = 0; i < e; ++i) idx[i] = i;
+        while (true) {
+            std::fill(er.begin(), er.end(), 0);
+            for (int v : idx) er[v] = 1;
+            int err = RS_OK;
+            if (pattern_for(c, er.data(), &err) < 0) return err;
+            int i = e - 1;
+            while (i >= 0 && idx[i] == c->n - e + i) --i;
+            if (i < 0) break;
+            ++idx[i];
+            for (int j = i + 1; j < e; ++j) idx[j] = idx[j - 1] + 1;
+        }
+    }
+    int st = upload_patterns(c, static_cast<hipStream_t>(stream));
+    if (st != RS_OK) return st;
+    return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
+int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, size_t pss,
+                      size_t pitch, size_t len, size_t stripes, void* stream) {
+    if (!c) return RS_EINVAL;
+    if (c->m == 0 || stripes == 0 || len == 0) return RS_OK;
+    if (!check_stripes_args(c, data, dss, parity, pss, pitch, len)) return RS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    rsmi::MatArgs a = base_args(c, const_cast<void*>(data), dss, parity, pss, pitch, len, stripes);
+    set_patterns(c, 1, c->d_encpat.p, a);
+    a.stripe_pat = nullptr;
+    return hip_status(rsmi::launch_matmul(a, c->m, static_cast<hipStream_t>(stream)));
+}
+
+int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
+                           size_t pitch, size_t len, size_t stripes, const uint8_t* erased,
+                           void* stream) {
+    if (!c || !erased) return RS_EINVAL;
+    if (stripes == 0 || len == 0) return RS_OK;
+    if (!check_stripes_args(c, data, dss, parity, pss, pitch, len)) return RS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!c->st_stripe.acquire(stripes * sizeof(uint32_t))) return RS_ENOMEM;
+    uint32_t* ids = static_cast<uint32_t*>(c->st_stripe.p);
+    int max_e = 0;
+    for (size_t i = 0; i < stripes; ++i) {
+        int err = RS_OK;
+        int id = pattern_for(c, erased + i * c->n, &err);
+        if (id < 0) return err;
+        ids[i] = static_cast<uint32_t>(id);
+        max_e = std::max<int>(max_e, c->h_cnt[id]);
+    }
+    if (max_e == 0) return RS_OK;  // nothing erased anywhere
+    int st = upload_patterns(c, s);
+    if (st != RS_OK) return st;
+    if (!c->d_stripe_pat.reserve(stripes * sizeof(uint32_t))) return RS_ENOMEM;
+    hipError_t e = hipMemcpyAsync(c->d_stripe_pat.p, ids, stripes * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, s);
+    c->st_stripe.release_after(s);
+    if (e != hipSuccess) return RS_EDEVICE;
+    rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, stripes);
+    set_patterns(c, c->h_cnt.size(), c->d_pats.p, a);
+    a.stripe_pat = static_cast<const uint32_t*>(c->d_stripe_pat.p);
+    return hip_status(rsmi::launch_matmul(a, max_e, s));
+}
+
+int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
+    if (!c) return RS_EINVAL;
+    if (len % static_cast<size_t>(c->k) != 0) return RS_ELEN_NOT_MULTIPLE;
+    const size_t S = len / static_cast<size_t>(c->k);
+    if (S == 0 || c->m == 0) return RS_OK;
+    if (!input || !parity) return RS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    const size_t pitch = round_up(S, 256);
+    if (round_up(S, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;
+    if (!c->d_work.reserve(pitch * static_cast<size_t>(c->n))) return RS_ENOMEM;
+    uint8_t* din = static_cast<uint8_t*>(c->d_work.p);
+    uint8_t* dpar = din + pitch * c->k;
+    hipStream_t s = c->stream;
+    hipError_t e = hipMemcpy2DAsync(din, pitch, input, S, S, c->k, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return RS_EDEVICE;
+    rsmi::MatArgs a = base_args(c, din, 0, dpar, 0, pitch, S, 1);
+    set_patterns(c, 1, c->d_encpat.p, a);
+    e = rsmi::launch_matmul(a, c->m, s);
+    if (e == hipSuccess) e = hipMemcpy2DAsync(parity, S, dpar, pitch, S, c->m, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return hip_status(e);
+}
+
+int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t share_len,
+              uint8_t* dst) {
+    if (!c) return RS_EINVAL;
+    const int k = c->k, n = c->n;
+    if (count < k) return RS_ENOT_ENOUGH;  // Correct: NotEnoughShares comes first
+    if (count <= 0) return RS_ENO_SHARES;
+    if (!numbers || !shares || (!dst && share_len)) return RS_EINVAL;
+    for (int i = 0; i < count; ++i)
+        if (numbers[i] < 0 || numbers[i] >= n) return RS_EBAD_SHARE_ID;
+    // sort.Sort(byNumber(shares)): in place on the caller's arrays.
+    std::vector<int> order(count);
+    for (int i = 0; i < count; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return numbers[a] < numbers[b]; });
+    std::vector<int> nums(count);
+    std::vector<const uint8_t*> ptrs(count);
+    for (int i = 0; i < count; ++i) {
+        nums[i] = numbers[order[i]];
+        ptrs[i] = shares[order[i]];
+    }
+    std::copy(nums.begin(), nums.end(), numbers);
+    std::copy(ptrs.begin(), ptrs.end(), shares);
+    std::vector<uint8_t> present(n, 0);
+    std::vector<const uint8_t*> by_id(n, nullptr);
+    int distinct = 0;
+    for (int i = 0; i < count; ++i)
+        if (!present[nums[i]]) {
+            present[nums[i]] = 1;
+            by_id[nums[i]] = ptrs[i];
+            ++distinct;
+        }
+    if (distinct < k) return RS_ESINGULAR;  // duplicate numbers: singular decode matrix
+    if (share_len == 0) return RS_OK;
+    for (int i = 0; i < n; ++i)
+        if (present[i] && !by_id[i]) return RS_EINVAL;
+    std::vector<int> surv = rsmi::choose_survivors(present.data(), k, n);
+    std::vector<int> missing;
+    for (int i = 0; i < k; ++i) {
+        if (present[i])
+            std::memcpy(dst + static_cast<size_t>(i) * share_len, by_id[i], share_len);
+        else
+            missing.push_back(i);
+    }
+    if (missing.empty()) return RS_OK;
+    std::vector<uint8_t> rows;
+    if (!rsmi::decode_rows(c->enc, k, n, surv, missing, rows)) return RS_ESINGULAR;
+
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    const int e = static_cast<int>(missing.size());
+    const size_t pitch = round_up(share_len, 256);
+    if (round_up(share_len, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;
+    if (!c->d_work.reserve(pitch * static_cast<size_t>(k + e))) return RS_ENOMEM;
+    uint8_t* din = static_cast<uint8_t*>(c->d_work.p);
+    uint8_t* dout = din + pitch * k;
+    // One-pattern table: coef rows, src = slots 0..k-1, dst = k..k+e-1.
+    std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
+    std::copy(rows.begin(), rows.end(), coef.begin());
+    std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(e));
+    for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
+    for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
+    const size_t patbytes = PatLayout(c, 1).total;
+    if (!c->d_onepat.reserve(patbytes) || !c->st_one.acquire(patbytes)) return RS_ENOMEM;
+    uint8_t* hp = static_cast<uint8_t*>(c->st_one.p);
+    pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp);
+    hipStream_t s = c->stream;
+    hipError_t err = hipMemcpyAsync(c->d_onepat.p, hp, patbytes, hipMemcpyHostToDevice, s);
+    for (int i = 0; i < k && err == hipSuccess; ++i)
+        err = hipMemcpyAsync(din + pitch * i, by_id[surv[i]], share_len, hipMemcpyHostToDevice, s);
+    c->st_one.release_after(s);
+    if (err != hipSuccess) return RS_EDEVICE;
+    rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, share_len, 1);
+    set_patterns(c, 1, c->d_onepat.p, a);
+    err = rsmi::launch_matmul(a, e, s);
+    for (int t = 0; t < e && err == hipSuccess; ++t)
+        err = hipMemcpyAsync(dst + static_cast<size_t>(missing[t]) * share_len, dout + pitch * t,
+                             share_len, hipMemcpyDeviceToHost, s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    return hip_status(err);
+}
+
+void* rs_pinned_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void rs_pinned_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int rs_device_alloc(rs_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return RS_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    return hipMalloc(out, bytes ? bytes : 1) == hipSuccess ? RS_OK : RS_ENOMEM;
+}
+
+int rs_device_free(rs_ctx* c, void* p) {
+    if (!c) return RS_EINVAL;
+    DeviceGuard g(c->device);
+    return hip_status(hipFree(p));
+}
+
+int rs_stream_sync(rs_ctx* c, void* stream) {
+    if (!c) return RS_EINVAL;
+    DeviceGuard g(c->device);
+    return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
+int rs_fill_splitmix(rs_ctx* c, void* dev, size_t len, uint64_t seed, void* stream) {
+    if (!c || (!dev && len)) return RS_EINVAL;
+    if (reinterpret_cast<uintptr_t>(dev) & 7u) return RS_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    return hip_status(rsmi::launch_fill_splitmix(dev, len, seed, static_cast<hipStream_t>(stream)));
+}
+
+}  // extern "C"

@@ -1,0 +1,260 @@
+"""ctypes binding of the MI355X Reed-Solomon engine (include/rsmi.h).
+
+Mirrors the github.com/vivint/infectious API the reference plugin calls
+(/root/reference/main.go:24 import, :73/:248 NewFEC, :262 Encode, :77 Decode,
+:57-69/:254-258 Share + DeepCopy) so Python callers and the tests read like
+the plugin.  The shared library lib/librsmi.so is built in-tree by
+``__graft_entry__.build()`` (or ``make -C noise-erasurecode-plugin_amd/csrc``);
+importing this module without it raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librsmi.so")
+
+# rs_status codes (include/rsmi.h)
+RS_OK = 0
+RS_EINVAL_KN = -1
+RS_ELEN_NOT_MULTIPLE = -2
+RS_ENOT_ENOUGH = -3
+RS_EBAD_SHARE_ID = -4
+RS_ESINGULAR = -5
+RS_ENO_SHARES = -6
+RS_ESHARE_LEN = -7
+RS_EINVAL = -8
+RS_EDEVICE = -9
+RS_ENOMEM = -10
+
+# Every symbol include/rsmi.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = (
+    "rs_new", "rs_new_on_device", "rs_free", "rs_k", "rs_n", "rs_device",
+    "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode",
+    "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_prepare_patterns",
+    "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
+    "rs_stream_sync", "rs_fill_splitmix",
+)
+
+
+class RSError(Exception):
+    """Error from the engine; .code is the rs_status value."""
+
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _lib().rs_strerror(code).decode() if _LIB is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+class NotEnoughShares(RSError):
+    """infectious NotEnoughShares (Rebuild/Correct with fewer than k shares)."""
+
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def _lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                "(the engine has no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        sig = {
+            "rs_new": (i32, [i32, i32, ctypes.POINTER(vp)]),
+            "rs_new_on_device": (i32, [i32, i32, i32, ctypes.POINTER(vp)]),
+            "rs_free": (None, [vp]),
+            "rs_k": (i32, [vp]),
+            "rs_n": (i32, [vp]),
+            "rs_device": (i32, [vp]),
+            "rs_encode_matrix": (i32, [vp, u8p]),
+            "rs_strerror": (ctypes.c_char_p, [i32]),
+            "rs_encode": (i32, [vp, vp, sz, vp]),
+            "rs_decode": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(vp), i32, sz, vp]),
+            "rs_encode_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp]),
+            "rs_reconstruct_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp, vp]),
+            "rs_pattern_count": (i32, [vp]),
+            "rs_prepare_patterns": (i32, [vp, i32, vp]),
+            "rs_pinned_alloc": (vp, [sz]),
+            "rs_pinned_free": (None, [vp]),
+            "rs_device_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
+            "rs_device_free": (i32, [vp, vp]),
+            "rs_stream_sync": (i32, [vp, vp]),
+            "rs_fill_splitmix": (i32, [vp, vp, sz, ctypes.c_uint64, vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = lib
+    return _LIB
+
+
+def load() -> ctypes.CDLL:
+    """The loaded engine library (raises ImportError if it was not built)."""
+    return _lib()
+
+
+def _check(code: int, what: str) -> None:
+    if code == RS_OK:
+        return
+    if code == RS_ENOT_ENOUGH:
+        raise NotEnoughShares(code, what)
+    raise RSError(code, what)
+
+
+@dataclass
+class Share:
+    """infectious.Share{Number int; Data []byte} (main.go:57-69, :254-258)."""
+
+    Number: int
+    Data: bytes
+
+    def DeepCopy(self) -> "Share":
+        return Share(self.Number, bytes(self.Data))
+
+
+class FEC:
+    """Handle of an rs_ctx: the engine-side infectious *FEC for (k, n)."""
+
+    def __init__(self, k: int, n: int, device: Optional[int] = None):
+        lib = _lib()
+        h = ctypes.c_void_p()
+        if device is None:
+            code = lib.rs_new(k, n, ctypes.byref(h))
+        else:
+            code = lib.rs_new_on_device(k, n, device, ctypes.byref(h))
+        _check(code, f"NewFEC({k}, {n})")
+        self._h = h
+        self.k = k
+        self.n = n
+
+    # -- infectious accessors -------------------------------------------------
+    def Required(self) -> int:
+        return self.k
+
+    def Total(self) -> int:
+        return self.n
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib().rs_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def matrix(self) -> bytes:
+        buf = (ctypes.c_uint8 * (self.n * self.k))()
+        _check(_lib().rs_encode_matrix(self._h, buf), "rs_encode_matrix")
+        return bytes(buf)
+
+    # -- (*FEC).Encode (main.go:262) ------------------------------------------
+    def Encode(self, input: bytes, output: Callable[[Share], None]) -> None:
+        """Calls output(Share) for shares 0..n-1 in order; like infectious,
+        data shares are views of input and the parity buffer is reused
+        between callbacks (callers DeepCopy, main.go:255-258)."""
+        data = bytes(input)
+        if len(data) % self.k != 0:
+            raise RSError(RS_ELEN_NOT_MULTIPLE, "Encode")
+        S = len(data) // self.k
+        m = self.n - self.k
+        parity = bytearray(m * S)
+        if S and m:
+            src = ctypes.c_char_p(data)
+            dst = (ctypes.c_char * len(parity)).from_buffer(parity)
+            _check(_lib().rs_encode(self._h, ctypes.cast(src, ctypes.c_void_p), len(data),
+                                    ctypes.cast(dst, ctypes.c_void_p)), "Encode")
+        view = memoryview(data)
+        for i in range(self.k):
+            output(Share(i, view[i * S:(i + 1) * S]))
+        pv = memoryview(parity)
+        for i in range(m):
+            output(Share(self.k + i, pv[i * S:(i + 1) * S]))
+
+    def encode_parity(self, input: bytes) -> bytes:
+        """Parity shares k..n-1 concatenated (rs_encode)."""
+        out: List[bytes] = []
+        self.Encode(input, lambda s: out.append(bytes(s.Data)) if s.Number >= self.k else None)
+        return b"".join(out)
+
+    # -- (*FEC).Decode (main.go:77) -------------------------------------------
+    def Decode(self, dst: Optional[bytearray], shares: List[Share]) -> bytes:
+        """Returns the k*S-byte original.  Sorts `shares` in place by Number,
+        as infectious does to the caller's slice."""
+        cnt = len(shares)
+        S = len(shares[0].Data) if cnt else 0
+        for s in shares:
+            if len(s.Data) != S:
+                raise RSError(RS_ESHARE_LEN, "Decode")
+        nums = (ctypes.c_int * max(cnt, 1))(*[s.Number for s in shares])
+        keep = [bytes(s.Data) for s in shares]
+        ptrs = (ctypes.c_void_p * max(cnt, 1))(
+            *[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value for b in keep])
+        out = bytearray(self.k * S)
+        outp = (ctypes.c_char * max(len(out), 1)).from_buffer(out) if out else None
+        code = _lib().rs_decode(self._h, nums, ptrs, cnt, S,
+                                ctypes.cast(outp, ctypes.c_void_p) if outp is not None else None)
+        _check(code, "Decode")
+        # mirror the in-place sort
+        order = sorted(range(cnt), key=lambda i: (shares[i].Number, i))
+        shares[:] = [shares[i] for i in order]
+        if dst is not None and len(dst) >= len(out):
+            dst[:len(out)] = out
+            return bytes(dst[:len(out)])
+        return bytes(out)
+
+    # -- device-resident batched API -------------------------------------------
+    def encode_stripes(self, data_ptr: int, data_stride: int, parity_ptr: int,
+                       parity_stride: int, pitch: int, shard_len: int, stripes: int,
+                       stream: int = 0) -> None:
+        _check(_lib().rs_encode_stripes(self._h, data_ptr, data_stride, parity_ptr,
+                                        parity_stride, pitch, shard_len, stripes,
+                                        stream or None), "rs_encode_stripes")
+
+    def reconstruct_stripes(self, data_ptr: int, data_stride: int, parity_ptr: int,
+                            parity_stride: int, pitch: int, shard_len: int, stripes: int,
+                            erased: bytes, stream: int = 0) -> None:
+        if len(erased) != stripes * self.n:
+            raise RSError(RS_EINVAL, "erased must hold stripes*n flags")
+        buf = ctypes.c_char_p(bytes(erased))
+        _check(_lib().rs_reconstruct_stripes(self._h, data_ptr, data_stride, parity_ptr,
+                                             parity_stride, pitch, shard_len, stripes,
+                                             ctypes.cast(buf, ctypes.c_void_p), stream or None),
+               "rs_reconstruct_stripes")
+
+    def pattern_count(self) -> int:
+        return _lib().rs_pattern_count(self._h)
+
+    def prepare_patterns(self, max_erasures: int, stream: int = 0) -> None:
+        _check(_lib().rs_prepare_patterns(self._h, max_erasures, stream or None),
+               "rs_prepare_patterns")
+
+    def fill_splitmix(self, dev_ptr: int, nbytes: int, seed: int, stream: int = 0) -> None:
+        _check(_lib().rs_fill_splitmix(self._h, dev_ptr, nbytes, seed & (2**64 - 1),
+                                       stream or None), "rs_fill_splitmix")
+
+    def sync(self, stream: int = 0) -> None:
+        _check(_lib().rs_stream_sync(self._h, stream or None), "rs_stream_sync")
+
+
+def NewFEC(k: int, n: int) -> FEC:
+    """infectious.NewFEC(k, n) (main.go:73, :248)."""
+    return FEC(k, n)
+
+
+def strerror(code: int) -> str:
+    return _lib().rs_strerror(code).decode()

@@ -1,0 +1,49 @@
+"""CPU: the C-ABI library loads and exports every symbol include/rsmi.h
+declares; the product library does not link or embed the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT, gpu_available
+
+HEADER = os.path.join(ROOT, "include", "rsmi.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rs_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    import rsmi
+    lib = ctypes.CDLL(rsmi.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert sorted(rsmi.EXPORTS) == names
+
+
+def test_product_does_not_contain_oracle():
+    import rsmi
+    out = subprocess.run(["nm", "-D", rsmi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "orc_" not in out
+    ldd = subprocess.run(["ldd", rsmi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd
+
+
+def test_strerror_and_no_gpu_behaviour():
+    import rsmi
+    assert rsmi.strerror(rsmi.RS_EINVAL_KN) == "requires 1 <= k <= n <= 256"
+    with pytest.raises(rsmi.RSError) as ei:
+        rsmi.NewFEC(0, 4)
+    assert ei.value.code == rsmi.RS_EINVAL_KN
+    if not gpu_available():
+        # No CPU fallback: without a gfx950 device the engine refuses to start.
+        with pytest.raises(rsmi.RSError) as ei:
+            rsmi.NewFEC(10, 14)
+        assert ei.value.code == rsmi.RS_EDEVICE

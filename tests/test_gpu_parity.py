@@ -1,0 +1,281 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bit-exact comparisons on seeded inputs at sizes the oracle finishes in
+seconds, the golden vectors, and size-independent properties at full size
+(encode -> erase -> reconstruct round trips).  Reference call sites:
+Encode main.go:262 (shardInput main.go:243-267), Decode main.go:77.
+"""
+import hashlib
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import rsmi  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "rs_golden.json")
+_FECS = {}
+
+
+def fec(k, n):
+    if (k, n) not in _FECS:
+        _FECS[(k, n)] = rsmi.NewFEC(k, n)
+    return _FECS[(k, n)]
+
+
+def collect(f, data):
+    shares = [None] * f.Total()
+
+    def out(s):
+        shares[s.Number] = s.DeepCopy()  # main.go:255-258
+
+    f.Encode(data, out)
+    return shares
+
+
+# ---------------------------------------------------------------- encode ----
+CONFIGS = [(1, 1), (1, 2), (2, 3), (3, 5), (4, 6), (8, 14), (10, 14), (16, 20), (17, 49),
+           (64, 80), (64, 100), (100, 120), (200, 256), (255, 256)]
+
+
+@pytest.mark.parametrize("k,n", CONFIGS)
+@pytest.mark.parametrize("S", [1, 15, 16, 17, 4099])
+def test_encode_matches_oracle(k, n, S):
+    f = fec(k, n)
+    E = oracle.fec_matrix(k, n)
+    assert f.matrix() == E.tobytes()
+    data = oracle.splitmix_bytes(k * S, 31 * k + n + S).tobytes()
+    shares = collect(f, data)
+    for i in range(k):  # systematic: data shares are the input slices
+        assert bytes(shares[i].Data) == data[i * S:(i + 1) * S]
+    got = b"".join(bytes(shares[i].Data) for i in range(k, n))
+    assert got == oracle.encode(E, k, n, data)
+
+
+def test_encode_golden_vectors():
+    with open(GOLDEN) as fh:
+        g = json.load(fh)
+    for rec in g["encodings"]:
+        k, n, S = rec["k"], rec["n"], rec["S"]
+        data = oracle.splitmix_bytes(k * S, rec["seed"]).tobytes()
+        par = fec(k, n).encode_parity(data)
+        assert hashlib.sha256(par).hexdigest() == rec["parity_sha256"], (k, n, S)
+
+
+def test_encode_plugin_config1_blob():
+    # BASELINE config 1: 1 MiB blob zero-padded to 1,048,580 B, RS(10,4).
+    blob = oracle.splitmix_bytes(1 << 20, 0x5EED).tobytes() + b"\0" * 4
+    f = fec(10, 14)
+    assert f.encode_parity(blob) == oracle.encode(oracle.fec_matrix(10, 14), 10, 14, blob)
+
+
+def test_encode_errors_and_empty():
+    f = fec(4, 6)
+    with pytest.raises(rsmi.RSError) as ei:
+        f.Encode(b"abcde", lambda s: None)
+    assert ei.value.code == rsmi.RS_ELEN_NOT_MULTIPLE
+    got = collect(f, b"")
+    assert all(len(s.Data) == 0 for s in got)
+
+
+# ---------------------------------------------------------------- decode ----
+def _shards(k, n, S, seed):
+    data = oracle.splitmix_bytes(k * S, seed).tobytes()
+    par = oracle.encode(oracle.fec_matrix(k, n), k, n, data)
+    sh = [data[i * S:(i + 1) * S] for i in range(k)] + [par[i * S:(i + 1) * S] for i in range(n - k)]
+    return data, sh
+
+
+def test_decode_all_erasure_patterns_rs10_4():
+    k, n, S = 10, 14, 100
+    data, sh = _shards(k, n, S, 4242)
+    f = fec(k, n)
+    for e in range(0, n - k + 1):
+        for lost in itertools.combinations(range(n), e):
+            keep = [i for i in range(n) if i not in lost][-k:][::-1]
+            shares = [rsmi.Share(i, sh[i]) for i in keep]
+            assert f.Decode(None, shares) == data, lost
+            assert [s.Number for s in shares] == sorted(keep)  # sorted in place
+
+
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 14), (17, 49), (64, 80), (200, 256)])
+def test_decode_matches_oracle(k, n):
+    rng = np.random.default_rng(k * 1000 + n)
+    S = 333
+    data, sh = _shards(k, n, S, k + n)
+    f = fec(k, n)
+    E = oracle.fec_matrix(k, n)
+    for _ in range(4):
+        keep = sorted(rng.choice(n, size=k, replace=False).tolist())
+        rng.shuffle(keep)
+        rc, ref = oracle.decode(E, k, n, [(i, sh[i]) for i in keep])
+        assert rc == 0 and ref == data
+        assert f.Decode(None, [rsmi.Share(i, sh[i]) for i in keep]) == ref
+
+
+def test_decode_more_than_k_shares():
+    k, n, S = 4, 6, 64
+    data, sh = _shards(k, n, S, 5)
+    assert fec(k, n).Decode(None, [rsmi.Share(i, sh[i]) for i in (5, 1, 4, 2, 3)]) == data
+
+
+def test_decode_errors():
+    k, n, S = 4, 6, 16
+    data, sh = _shards(k, n, S, 6)
+    f = fec(k, n)
+    with pytest.raises(rsmi.NotEnoughShares):
+        f.Decode(None, [rsmi.Share(i, sh[i]) for i in range(3)])
+    with pytest.raises(rsmi.RSError) as ei:
+        f.Decode(None, [rsmi.Share(i, sh[i]) for i in (0, 1, 2)] + [rsmi.Share(7, sh[3])])
+    assert ei.value.code == rsmi.RS_EBAD_SHARE_ID
+    with pytest.raises(rsmi.RSError) as ei:
+        f.Decode(None, [rsmi.Share(i, sh[i]) for i in (0, 0, 1, 2)])
+    assert ei.value.code == rsmi.RS_ESINGULAR
+    with pytest.raises(rsmi.RSError) as ei:
+        f.Decode(None, [rsmi.Share(0, sh[0]), rsmi.Share(1, sh[1][:5]), rsmi.Share(2, sh[2]),
+                        rsmi.Share(3, sh[3])])
+    assert ei.value.code == rsmi.RS_ESHARE_LEN
+
+
+# ------------------------------------------------------- batched (device) ----
+def _dev_stripes(f, stripes, S, pitch, seed):
+    k, m = f.k, f.n - f.k
+    data = torch.empty(stripes * k * pitch, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(data.data_ptr(), data.numel(), seed)
+    parity = torch.zeros(stripes * m * pitch, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    return data, parity
+
+
+@pytest.mark.parametrize("k,n,S,pitch", [(10, 14, 65536, 65536), (10, 14, 1000, 1024),
+                                         (4, 6, 4096, 4096), (64, 80, 65536, 65536),
+                                         (17, 49, 4000, 4096), (8, 14, 100, 112)])
+def test_encode_stripes_matches_oracle(k, n, S, pitch):
+    f = fec(k, n)
+    m = n - k
+    stripes = 7
+    data, parity = _dev_stripes(f, stripes, S, pitch, 77 + k)
+    f.encode_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes)
+    f.sync()
+    hd = data.cpu().numpy().reshape(stripes, k, pitch)
+    hp = parity.cpu().numpy().reshape(stripes, m, pitch)
+    E = oracle.fec_matrix(k, n)
+    for s in range(stripes):
+        ref = oracle.encode(E, k, n, hd[s, :, :S].tobytes())
+        assert hp[s, :, :S].tobytes() == ref, s
+
+
+def test_fill_splitmix_matches_oracle():
+    f = fec(10, 14)
+    for n_bytes in (1, 7, 8, 4099, 1 << 16):
+        t = torch.empty(n_bytes + 8, dtype=torch.uint8, device="cuda")
+        f.fill_splitmix(t.data_ptr(), n_bytes, 1234)
+        f.sync()
+        assert t[:n_bytes].cpu().numpy().tobytes() == oracle.splitmix_bytes(n_bytes, 1234).tobytes()
+
+
+def _erasures(rng, stripes, n, m, emin=1, emax=None):
+    emax = m if emax is None else emax
+    er = np.zeros((stripes, n), dtype=np.uint8)
+    for s in range(stripes):
+        e = int(rng.integers(emin, emax + 1))
+        er[s, rng.choice(n, size=e, replace=False)] = 1
+    return er
+
+
+@pytest.mark.parametrize("k,n,S,pitch,stripes", [(10, 14, 65536, 65536, 64),
+                                                 (10, 14, 999, 1008, 50),
+                                                 (4, 6, 4096, 4096, 40),
+                                                 (64, 80, 65536, 65536, 6),
+                                                 (17, 49, 4000, 4096, 9)])
+def test_reconstruct_stripes_roundtrip(k, n, S, pitch, stripes):
+    f = fec(k, n)
+    m = n - k
+    rng = np.random.default_rng(k + n + S)
+    data, parity = _dev_stripes(f, stripes, S, pitch, 900 + k)
+    f.encode_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes)
+    f.sync()
+    d0, p0 = data.clone(), parity.clone()
+    er = _erasures(rng, stripes, n, m)
+    dv = data.view(stripes, k, pitch)
+    pv = parity.view(stripes, m, pitch)
+    for s in range(stripes):  # destroy the erased shards
+        for i in np.nonzero(er[s])[0]:
+            (dv[s, i] if i < k else pv[s, i - k]).fill_(0xA5)
+    f.reconstruct_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S,
+                          stripes, er.tobytes())
+    f.sync()
+    dv0, pv0 = d0.view(stripes, k, pitch), p0.view(stripes, m, pitch)
+    assert torch.equal(dv[:, :, :S], dv0[:, :, :S])
+    assert torch.equal(pv[:, :, :S], pv0[:, :, :S])
+
+
+def test_reconstruct_too_many_erasures_rejected():
+    f = fec(4, 6)
+    data, parity = _dev_stripes(f, 2, 256, 256, 1)
+    er = np.zeros((2, 6), dtype=np.uint8)
+    er[1, :3] = 1
+    with pytest.raises(rsmi.NotEnoughShares):
+        f.reconstruct_stripes(data.data_ptr(), 4 * 256, parity.data_ptr(), 2 * 256, 256, 256, 2,
+                              er.tobytes())
+
+
+def test_reconstruct_matches_oracle_rows():
+    """Regenerated shards equal the oracle's Rebuild of the same survivors."""
+    k, n, S, stripes = 10, 14, 4096, 12
+    f = fec(k, n)
+    m = n - k
+    rng = np.random.default_rng(3)
+    data, parity = _dev_stripes(f, stripes, S, S, 55)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    er = _erasures(rng, stripes, n, m, emin=4, emax=4)
+    hd = data.cpu().numpy().reshape(stripes, k, S)
+    hp = parity.cpu().numpy().reshape(stripes, m, S)
+    E = oracle.fec_matrix(k, n)
+    for s in range(stripes):
+        sh = [hd[s, i].tobytes() for i in range(k)] + [hp[s, i].tobytes() for i in range(m)]
+        keep = [i for i in range(n) if not er[s, i]]
+        rc, ref = oracle.decode(E, k, n, [(i, sh[i]) for i in keep[:k]])
+        assert rc == 0 and ref == hd[s].tobytes()
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                          er.tobytes())
+    f.sync()
+    assert data.cpu().numpy().reshape(stripes, k, S).tobytes() == hd.tobytes()
+
+
+def test_full_size_rs10_4_roundtrip():
+    """BASELINE geometry (1 MiB shards), 256 stripes: encode, spot-check
+    parity against the oracle, erase 1-4 shards per stripe, reconstruct,
+    compare everything on the device."""
+    k, n, S, stripes = 10, 14, 1 << 20, 256
+    f = fec(k, n)
+    m = n - k
+    data, parity = _dev_stripes(f, stripes, S, S, 0x5EED)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    E = oracle.fec_matrix(k, n)
+    for s in (0, 131, 255):
+        hd = data[s * k * S:(s + 1) * k * S].cpu().numpy().tobytes()
+        hp = parity[s * m * S:(s + 1) * m * S].cpu().numpy().tobytes()
+        assert hp == oracle.encode(E, k, n, hd)
+    d0, p0 = data.clone(), parity.clone()
+    er = _erasures(np.random.default_rng(0xE4A5), stripes, n, m)
+    erd = torch.from_numpy(er[:, :k].astype(bool)).cuda()
+    erp = torch.from_numpy(er[:, k:].astype(bool)).cuda()
+    data.view(stripes, k, S)[erd] = 0
+    parity.view(stripes, m, S)[erp] = 0
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                          er.tobytes())
+    f.sync()
+    assert torch.equal(data, d0)
+    assert torch.equal(parity, p0)
