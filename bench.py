@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--emin", type=int, default=1)
     ap.add_argument("--emax", type=int, default=None)
     ap.add_argument("--mode", choices=["both", "encode", "reconstruct"], default="both")
+    ap.add_argument("--erase", default=None,
+                    help="fixed erased shard ids for every stripe, e.g. 0,1,2,3 (default random)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
@@ -136,7 +138,12 @@ def main():
     f.fill_splitmix(parity.data_ptr(), parity.numel(), 1, sh)
     f.prepare_patterns(emax, sh)
     rng = np.random.default_rng(0xE4A5 + rank)
-    ersets = erasure_sets(rng, args.warmup + args.steps, stripes, n, args.emin, emax)
+    if args.erase:
+        fixed = np.zeros((stripes, n), dtype=np.uint8)
+        fixed[:, [int(v) for v in args.erase.split(",")]] = 1
+        ersets = [fixed] * (args.warmup + args.steps)
+    else:
+        ersets = erasure_sets(rng, args.warmup + args.steps, stripes, n, args.emin, emax)
     rec_bytes = [int(((k + er.sum(axis=1)) * S).sum()) for er in ersets]
     enc_bytes = stripes * (k + m) * S
 

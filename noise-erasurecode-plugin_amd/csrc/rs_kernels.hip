@@ -17,6 +17,7 @@
 #include "rs_kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace rsmi {
 namespace {
@@ -148,18 +149,31 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
     b /= a.groups;
     const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);
     const uint64_t s = b / a.chunks;
-    const uint32_t pat = __builtin_amdgcn_readfirstlane(a.stripe_pat ? a.stripe_pat[s] : 0u);
-    const int e = static_cast<int>(__builtin_amdgcn_readfirstlane(a.cnt[pat]));
+    // Stripe word = pattern id << 8 | outputs (one dependent load); encode
+    // (no stripe table) is pattern 0 with all m parity rows.
+    const uint32_t sw = __builtin_amdgcn_readfirstlane(a.stripe_pat ? a.stripe_pat[s] : a.m);
+    const uint32_t pat = sw >> 8;
+    const int e = static_cast<int>(sw & 0xFFu);
     const int row0 = static_cast<int>(grp) * MG;
     if (row0 >= e) return;  // whole block: uniform
     const int eg = min(MG, e - row0);
+
+    // This lane's coefficient byte for the table build is requested first, so
+    // waiting for it later does not wait for the survivor loads behind it.
+    const uint8_t* coef = a.coef + (static_cast<size_t>(pat) * a.m + row0) * k;
+    uint32_t cbyte[(K > 0 && K * MG <= kBlock) ? 1 : 1];
+    const bool one_coef = (K > 0 && K * MG <= kBlock);
+    if (one_coef) {
+        const int j = threadIdx.x / MG, t = threadIdx.x - j * MG;
+        cbyte[0] = (static_cast<int>(threadIdx.x) < k * MG && t < eg) ? coef[t * k + j] : 0u;
+    }
 
     auto shard = [&](uint32_t id) -> uint8_t* {
         return id < a.k ? a.data + s * a.data_ss + static_cast<uint64_t>(id) * a.pitch
                         : a.parity + s * a.parity_ss + static_cast<uint64_t>(id - a.k) * a.pitch;
     };
     const uint32_t* srcid = a.src + static_cast<size_t>(pat) * k;
-    const uint32_t* dstid = a.dst + static_cast<size_t>(pat) * a.m + row0;
+    const uint32_t* dstid = a.dst + static_cast<size_t>(pat) * a.dst_stride + row0;
     uint8_t* sp[kRegPtrs ? K : 1];
     if constexpr (kRegPtrs) {
 #pragma unroll
@@ -167,21 +181,45 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
     } else {
         for (int i = threadIdx.x; i < k; i += kBlock) sptr[i] = shard(srcid[i]);
     }
+    const uint32_t last = a.ncols16 - 1;
+    // Survivor loads of the block's first iteration are issued before the
+    // table build, so the prologue (pattern lookup, tables, barrier) overlaps
+    // their HBM latency; with one iteration per block (the default) this is
+    // the whole data path.
+    uint4 xpre[kRegPtrs ? K : 1];
+    const uint32_t col0 = chunk * a.iters * kBlock + threadIdx.x;
+    const uint32_t off0 = (col0 <= last ? col0 : last) * 16u;
+    if constexpr (kRegPtrs) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) xpre[j] = gload16(sp[j] + off0);
+    }
+    // Output pointers are only needed at store time.  Rows are padded to 16
+    // ids, so whole 4-id groups load unconditionally (s_load_dwordx4); rows
+    // past eg point at a valid shard and are never stored.
     uint8_t* dp[MG];
 #pragma unroll
-    for (int t = 0; t < MG; ++t)
-        dp[t] = t < eg ? uniform_ptr(shard(__builtin_amdgcn_readfirstlane(dstid[t]))) : nullptr;
+    for (int g = 0; g < MG / 4; ++g) {
+        const uint4 ids = *reinterpret_cast<const uint4*>(dstid + 4 * g);
+        const uint32_t idv[4] = {ids.x, ids.y, ids.z, ids.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dp[4 * g + r] = uniform_ptr(shard(__builtin_amdgcn_readfirstlane(idv[r])));
+    }
     // Split tables of rows [row0, row0 + MG): sub-step (j, g) holds rows
     // 4g..4g+3 as 4 x 5 dwords.
-    const uint8_t* coef = a.coef + (static_cast<size_t>(pat) * a.m + row0) * k;
-    for (int idx = threadIdx.x; idx < k * MG; idx += kBlock) {
-        const int j = idx / MG, t = idx - j * MG;
-        const uint32_t c = (t < eg) ? coef[t * k + j] : 0u;
-        build_tables(c, &tw[(j * TG + t / kRowsPerStep) * kStepWords + (t % kRowsPerStep) * 5]);
+    if (one_coef) {
+        if (static_cast<int>(threadIdx.x) < k * MG) {
+            const int j = threadIdx.x / MG, t = threadIdx.x - j * MG;
+            build_tables(cbyte[0], &tw[(j * TG + t / kRowsPerStep) * kStepWords + (t % kRowsPerStep) * 5]);
+        }
+    } else {
+        for (int idx = threadIdx.x; idx < k * MG; idx += kBlock) {
+            const int j = idx / MG, t = idx - j * MG;
+            const uint32_t c = (t < eg) ? coef[t * k + j] : 0u;
+            build_tables(c, &tw[(j * TG + t / kRowsPerStep) * kStepWords + (t % kRowsPerStep) * 5]);
+        }
     }
     __syncthreads();
 
-    const uint32_t last = a.ncols16 - 1;
     for (uint32_t it = 0; it < a.iters; ++it) {
         const uint32_t colbase = (chunk * a.iters + it) * kBlock;
         if (colbase >= a.ncols16) break;
@@ -197,14 +235,18 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
             for (int r = 0; r < kRowsPerStep; ++r)
 #pragma unroll
                 for (int w = 0; w < 4; ++w) acc[g][r][w] = 0u;
+        // Row groups of 4 beyond the pattern's outputs are skipped (uniform).
+        const int tg_used = (eg + kRowsPerStep - 1) / kRowsPerStep;
 
         for (int jb = 0; jb < k; jb += JB) {
-            uint4 x[JB];
+            uint4 xb[kRegPtrs ? 1 : JB];
+            uint4* x = kRegPtrs ? xpre : xb;
+            if constexpr (!kRegPtrs) {
 #pragma unroll
-            for (int q = 0; q < JB; ++q) {
-                if (K == 0 && jb + q >= k) break;
-                const uint8_t* base = kRegPtrs ? sp[kRegPtrs ? jb + q : 0] : uniform_ptr(sptr[jb + q]);
-                x[q] = gload16(base + off);
+                for (int q = 0; q < JB; ++q) {
+                    if (K == 0 && jb + q >= k) break;
+                    x[q] = gload16(uniform_ptr(sptr[jb + q]) + off);
+                }
             }
             uint32_t TA[kStepWords], TB[kStepWords];
             load_step(lds4 + static_cast<size_t>(jb * TG) * (kStepWords / 4), TA);
@@ -219,11 +261,21 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
                     const int step = (jb + q) * TG + g;
                     const bool more = (g + 1 < TG) || (q + 1 < JB && (K != 0 || jb + q + 1 < k));
                     if (more) load_step(lds4 + static_cast<size_t>(step + 1) * (kStepWords / 4), TB);
-                    mac_step(acc[g], x[q], TA);
+                    if (TG == 1 || g < tg_used) mac_step(acc[g], x[q], TA);
                     step_fence(acc[g]);
 #pragma unroll
                     for (int w = 0; w < kStepWords; ++w) TA[w] = TB[w];
                 }
+            }
+        }
+        if constexpr (kRegPtrs) {
+            // Software pipelining: the next iteration's survivor loads go out
+            // before this iteration's stores.
+            const uint32_t ncol = colbase + kBlock + threadIdx.x;
+            if (it + 1 < a.iters && colbase + kBlock < a.ncols16) {
+                const uint32_t noff = (ncol <= last ? ncol : last) * 16u;
+#pragma unroll
+                for (int j = 0; j < K; ++j) xpre[j] = gload16(sp[j] + noff);
             }
         }
 #pragma unroll
@@ -288,7 +340,12 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     if (a.stripes == 0 || a.ncols16 == 0 || max_e <= 0) return hipSuccess;
     const Variant& v = pick(static_cast<int>(a.k), static_cast<int>(a.m));
     const uint32_t total_it = (a.ncols16 + kBlock - 1) / kBlock;
-    a.iters = std::min<uint32_t>(16u, total_it);
+    static const uint32_t iters_cap = [] {
+        const char* e = std::getenv("RSMI_ITERS");  // tuning knob (default 1: one 4 KiB column chunk per block)
+        const int v = e ? std::atoi(e) : 1;
+        return static_cast<uint32_t>(v > 0 ? v : 1);
+    }();
+    a.iters = std::min<uint32_t>(iters_cap, total_it);
     a.chunks = (total_it + a.iters - 1) / a.iters;
     a.groups = static_cast<uint32_t>((max_e + v.MG - 1) / v.MG);
     const size_t lds = static_cast<size_t>(a.k) * v.MG * 5 * 4 + a.k * sizeof(void*);

@@ -11,6 +11,7 @@ namespace rsmi {
 // survivor shards src[pat][0..k-1] and writes the e = cnt[pat] output shards
 // dst[pat][0..e-1]:  out_t = sum_c coef[pat][t][c] * shard[src[pat][c]].
 // Encode is the single pattern {src = 0..k-1, dst = k..n-1, coef = E_bottom}.
+// Pattern p's outputs count lives in the stripe word (stripe_pat[s] & 0xFF).
 // Shard id i < k lives in the data region, i >= k in the parity region
 // (see rsmi.h, rs_encode_stripes).
 struct MatArgs {
@@ -27,9 +28,10 @@ struct MatArgs {
     uint32_t k, m;
     const uint8_t* coef;         // [npat][m][k]
     const uint32_t* src;         // [npat][k]   survivor shard ids
-    const uint32_t* dst;         // [npat][m]   output shard ids
-    const uint32_t* cnt;         // [npat]      outputs per pattern (<= m)
-    const uint32_t* stripe_pat;  // [stripes] pattern id, or nullptr: pattern 0
+    const uint32_t* dst;         // [npat][dst_stride] output shard ids (padded, >= 16)
+    uint32_t dst_stride;
+    const uint32_t* stripe_pat;  // [stripes] pattern id << 8 | outputs, or nullptr:
+                                 // pattern 0 with all m rows (encode)
 };
 
 // Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel

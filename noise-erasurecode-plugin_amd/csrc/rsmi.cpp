@@ -123,27 +123,36 @@ namespace {
 
 int hip_status(hipError_t e) { return e == hipSuccess ? RS_OK : RS_EDEVICE; }
 
+// Output ids per pattern are padded to a multiple of 16 so the kernel can
+// load a whole row group's ids unconditionally.
+size_t dst_stride(const rs_ctx* c) { return std::max<size_t>(16, round_up(c->m, 16)); }
+
 // Device blob of npat patterns: coef bytes [npat][m][k] (padded to 16) |
-// src u32 [npat][k] | dst u32 [npat][m] | cnt u32 [npat].
+// src u32 [npat][k] | dst u32 [npat][dst_stride] | sw u32 [npat], where
+// sw[p] = p << 8 | outputs is the stripe word of a stripe using pattern p.
 struct PatLayout {
-    size_t coef, src, dst, cnt, total;
+    size_t coef, src, dst, sw, total;
     PatLayout(const rs_ctx* c, size_t npat) {
         coef = 0;
         src = round_up(npat * c->m * c->k, 16);
         dst = src + npat * c->k * 4;
-        cnt = dst + npat * c->m * 4;
-        total = cnt + npat * 4;
+        sw = dst + npat * dst_stride(c) * 4;
+        total = sw + npat * 4;
     }
 };
 
 void pack_patterns(const rs_ctx* c, size_t npat, const uint8_t* coef, const uint32_t* src,
                    const uint32_t* dst, const uint32_t* cnt, uint8_t* out) {
     PatLayout L(c, npat);
+    const size_t ds = dst_stride(c);
     std::memset(out, 0, L.total);
     std::memcpy(out + L.coef, coef, npat * c->m * c->k);
     std::memcpy(out + L.src, src, npat * c->k * 4);
-    std::memcpy(out + L.dst, dst, npat * c->m * 4);
-    std::memcpy(out + L.cnt, cnt, npat * 4);
+    for (size_t p = 0; p < npat; ++p) {
+        std::memcpy(out + L.dst + p * ds * 4, dst + p * c->m, c->m * 4);
+        const uint32_t sw = static_cast<uint32_t>(p << 8) | cnt[p];
+        std::memcpy(out + L.sw + p * 4, &sw, 4);
+    }
 }
 
 void set_patterns(const rs_ctx* c, size_t npat, const void* dev, rsmi::MatArgs& a) {
@@ -152,7 +161,13 @@ void set_patterns(const rs_ctx* c, size_t npat, const void* dev, rsmi::MatArgs& 
     a.coef = b + L.coef;
     a.src = reinterpret_cast<const uint32_t*>(b + L.src);
     a.dst = reinterpret_cast<const uint32_t*>(b + L.dst);
-    a.cnt = reinterpret_cast<const uint32_t*>(b + L.cnt);
+    a.dst_stride = static_cast<uint32_t>(dst_stride(c));
+    a.stripe_pat = nullptr;
+}
+
+// Stripe word of pattern 0 of a blob (single-stripe launches with e < m).
+const uint32_t* first_stripe_word(const rs_ctx* c, const void* dev) {
+    return reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(dev) + PatLayout(c, 1).sw);
 }
 
 bool check_stripes_args(const rs_ctx* c, const void* data, size_t dss, const void* parity,
@@ -199,7 +214,7 @@ int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
         *err = RS_ENOT_ENOUGH;
         return -1;
     }
-    if (c->pat_index.size() >= (size_t(1) << 20)) {  // bound the cache: start over
+    if (c->pat_index.size() >= (size_t(1) << 20)) {  // bound the cache (ids are 24-bit): start over
         (void)hipDeviceSynchronize();
         c->pat_index.clear();
         c->h_coef.clear();
@@ -402,7 +417,7 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
         int err = RS_OK;
         int id = pattern_for(c, erased + i * c->n, &err);
         if (id < 0) return err;
-        ids[i] = static_cast<uint32_t>(id);
+        ids[i] = (static_cast<uint32_t>(id) << 8) | c->h_cnt[id];
         max_e = std::max<int>(max_e, c->h_cnt[id]);
     }
     if (max_e == 0) return RS_OK;  // nothing erased anywhere
@@ -517,6 +532,7 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (err != hipSuccess) return RS_EDEVICE;
     rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, share_len, 1);
     set_patterns(c, 1, c->d_onepat.p, a);
+    a.stripe_pat = first_stripe_word(c, c->d_onepat.p);  // e outputs, not m
     err = rsmi::launch_matmul(a, e, s);
     for (int t = 0; t < e && err == hipSuccess; ++t)
         err = hipMemcpyAsync(dst + static_cast<size_t>(missing[t]) * share_len, dout + pitch * t,

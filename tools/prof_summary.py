@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 profile of bench.py (tools/profile_*.sh layout).
+
+Reads <dir>/trace/run_kernel_trace.csv (+ run_kernel_stats.csv) and the
+separate PMC passes <dir>/fetch, <dir>/write (FETCH_SIZE / WRITE_SIZE, KiB),
+splits the rs_matmul launches by role (bench.py alternates encode and
+reconstruct launches in --mode both), applies the gfx950 correction from
+/opt/skills/guides/MI355X_MICROARCH.md §HBM (FETCH_SIZE reads exactly half the
+bytes of a wide coalesced streaming read: x2; WRITE_SIZE exact for 16-B
+stores) and writes a markdown summary plus profiles/traffic.json, which
+bench.py reports as roofline.traffic.
+
+usage: tools/prof_summary.py <profile dir> <out.md> [--stripes N --k K --n N --shard S]
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+
+def rows(path):
+    if not os.path.exists(path):
+        return []
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def matmul_only(rs):
+    return [r for r in rs if "rs_matmul_kernel" in r["Kernel_Name"]]
+
+
+def split_roles(rs, mode):
+    """bench --mode both: launches alternate encode, reconstruct."""
+    if mode == "both":
+        return {"encode": rs[0::2], "reconstruct": rs[1::2]}
+    return {mode: rs}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("out")
+    ap.add_argument("--mode", default="both")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--n", type=int, default=14)
+    ap.add_argument("--shard", type=int, default=1 << 20)
+    ap.add_argument("--stripes", type=int, default=6553)
+    ap.add_argument("--bench-log", default=None)
+    ap.add_argument("--traffic-json", default=None)
+    a = ap.parse_args()
+    k, n, S, st = a.k, a.n, a.shard, a.stripes
+    m = n - k
+    alg_enc = st * (k + m) * S
+
+    tr = matmul_only(rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv")))
+    roles = split_roles(tr, a.mode)
+    lines = [f"# rocprofv3 summary: {os.path.basename(os.path.normpath(a.dir))}", ""]
+    lines.append(f"Workload: RS({k},{n}), {st} stripes x {k} x {S} B shards, bench.py --mode {a.mode}.")
+    lines.append("")
+    lines.append("## Kernel trace (rocprofv3 --kernel-trace --stats)")
+    lines.append("")
+    stats = rows(os.path.join(a.dir, "trace", "run_kernel_stats.csv"))
+    lines.append("| kernel | calls | avg ms | min ms | max ms | % time |")
+    lines.append("|---|---|---|---|---|---|")
+    for r in stats:
+        lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
+                     f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} | {float(r['Percentage']):.2f} |")
+    lines.append("")
+    lines.append("Per role (launch order alternates encode / reconstruct):")
+    lines.append("")
+    lines.append("| role | launches | avg ms | VGPR | grid |")
+    lines.append("|---|---|---|---|---|")
+    avg = {}
+    for role, rs in roles.items():
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rs]
+        if not d:
+            continue
+        avg[role] = statistics.mean(d)
+        lines.append(f"| {role} | {len(d)} | {avg[role]:.3f} | {rs[0].get('VGPR_Count', '?')} | "
+                     f"{rs[0].get('Grid_Size', '?')} |")
+    lines.append("")
+
+    traffic = {}
+    pmc = {}
+    for cnt, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        rs = [r for r in matmul_only(rows(os.path.join(a.dir, sub, "run_counter_collection.csv")))
+              if r["Counter_Name"] == cnt]
+        pmc[cnt] = split_roles(rs, a.mode)
+    lines.append("## HBM traffic (separate --pmc passes, per launch)")
+    lines.append("")
+    lines.append("FETCH_SIZE x 1024 x 2 (gfx950: FETCH_SIZE counts half of a wide streaming read), "
+                 "WRITE_SIZE x 1024 (exact for 16-B stores).")
+    lines.append("")
+    lines.append("| role | FETCH_SIZE KiB | read GB (corrected) | WRITE_SIZE KiB | write GB | traffic GB | algorithmic GB | traffic / algorithmic |")
+    lines.append("|---|---|---|---|---|---|---|---|")
+    for role in roles:
+        f = [float(r["Counter_Value"]) for r in pmc["FETCH_SIZE"].get(role, [])]
+        w = [float(r["Counter_Value"]) for r in pmc["WRITE_SIZE"].get(role, [])]
+        if not f or not w:
+            continue
+        rd = statistics.mean(f) * 1024 * 2
+        wr = statistics.mean(w) * 1024
+        if role == "encode":
+            alg = alg_enc
+        else:
+            alg = None
+        t = rd + wr
+        traffic[f"{role}_k{k}_n{n}_S{S}_stripes{st}"] = round(t / 1e9, 3)
+        lines.append(f"| {role} | {statistics.mean(f):.0f} | {rd/1e9:.2f} | {statistics.mean(w):.0f} | "
+                     f"{wr/1e9:.2f} | {t/1e9:.2f} | {alg/1e9 if alg else float('nan'):.2f} | "
+                     f"{(t/alg) if alg else float('nan'):.3f} |")
+    lines.append("")
+    if "encode" in avg:
+        ach = alg_enc / (avg["encode"] / 1e3) / 1e9
+        lines.append(f"Encode: algorithmic {alg_enc/1e9:.2f} GB per launch / {avg['encode']:.3f} ms = "
+                     f"**{ach:.0f} GB/s = {ach/8000:.1%} of 8 TB/s**.")
+    if a.bench_log and os.path.exists(a.bench_log):
+        for line in open(a.bench_log):
+            if line.startswith("{"):
+                b = json.loads(line)
+                lines.append("")
+                lines.append(f"bench.py line of the profiled run: value {b['value']} GB/s, encode "
+                             f"{b['breakdown']['encode_ms']} ms (HIP events), reconstruct "
+                             f"{b['breakdown']['reconstruct_ms']} ms.")
+    with open(a.out, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    if a.traffic_json:
+        old = {}
+        if os.path.exists(a.traffic_json):
+            old = json.load(open(a.traffic_json))
+        old.update({key: v for key, v in traffic.items()})
+        old["_note"] = ("HBM GB per launch from rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                        "(tools/prof_summary.py)")
+        json.dump(old, open(a.traffic_json, "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
