@@ -1,0 +1,82 @@
+// infectious.cpp -- see infectious.hpp.
+#include "infectious.hpp"
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+
+#include "../../include/rsmi.h"
+
+namespace rsmi_host {
+
+std::string StatusText(int code) { return rs_strerror(code); }
+
+static Status from(int code, const char* what) {
+    if (code == RS_OK) return Status::Ok();
+    return Status::Err(code, std::string(what) + ": " + rs_strerror(code));
+}
+
+FEC::~FEC() {
+    if (ctx_) rs_free(ctx_);
+}
+
+Status NewFEC(int k, int n, std::shared_ptr<FEC>* out) {
+    rs_ctx* c = nullptr;
+    const int rc = rs_new(k, n, &c);
+    if (rc != RS_OK) return from(rc, "NewFEC");
+    out->reset(new FEC(k, n, c));
+    return Status::Ok();
+}
+
+Status CachedFEC(int k, int n, std::shared_ptr<FEC>* out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::shared_ptr<FEC>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({k, n});
+    if (it != cache.end()) {
+        *out = it->second;
+        return Status::Ok();
+    }
+    Status st = NewFEC(k, n, out);
+    if (st.ok()) cache[{k, n}] = *out;
+    return st;
+}
+
+Status FEC::Encode(const uint8_t* input, size_t len,
+                   const std::function<void(const ShareView&)>& output) {
+    if (len % static_cast<size_t>(k_) != 0)
+        return from(RS_ELEN_NOT_MULTIPLE, "Encode");
+    const size_t S = len / static_cast<size_t>(k_);
+    const int m = n_ - k_;
+    parity_.resize(static_cast<size_t>(m) * S);
+    if (S && m) {
+        const int rc = rs_encode(ctx_, input, len, parity_.data());
+        if (rc != RS_OK) return from(rc, "Encode");
+    }
+    for (int i = 0; i < k_; ++i) output(ShareView{i, input + static_cast<size_t>(i) * S, S});
+    for (int i = 0; i < m; ++i) output(ShareView{k_ + i, parity_.data() + static_cast<size_t>(i) * S, S});
+    return Status::Ok();
+}
+
+Status FEC::Decode(std::vector<uint8_t>* dst, std::vector<Share>& shares) {
+    const int cnt = static_cast<int>(shares.size());
+    const size_t S = cnt ? shares[0].Data.size() : 0;
+    for (const Share& s : shares)
+        if (s.Data.size() != S) return from(RS_ESHARE_LEN, "Decode");
+    std::vector<int> nums(cnt);
+    std::vector<const uint8_t*> ptrs(cnt);
+    for (int i = 0; i < cnt; ++i) {
+        nums[i] = shares[i].Number;
+        ptrs[i] = shares[i].Data.data();
+    }
+    std::vector<uint8_t> out(static_cast<size_t>(k_) * S);
+    const int rc = rs_decode(ctx_, nums.data(), ptrs.data(), cnt, S, out.data());
+    if (rc != RS_OK) return from(rc, "Decode");
+    // mirror infectious's in-place sort of the caller's slice
+    std::stable_sort(shares.begin(), shares.end(),
+                     [](const Share& a, const Share& b) { return a.Number < b.Number; });
+    *dst = std::move(out);
+    return Status::Ok();
+}
+
+}  // namespace rsmi_host

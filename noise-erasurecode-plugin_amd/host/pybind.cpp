@@ -1,0 +1,169 @@
+// pybind.cpp -- Python module _rsmi_host: the C++ host layer (infectious.hpp,
+// shard_plugin.hpp) for the tests and bench, so they drive the same C++ code
+// a native caller would.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "infectious.hpp"
+#include "shard_plugin.hpp"
+
+namespace py = pybind11;
+using namespace rsmi_host;
+
+namespace {
+
+std::vector<uint8_t> to_vec(const py::bytes& b) {
+    const std::string s = b;
+    return std::vector<uint8_t>(s.begin(), s.end());
+}
+py::bytes to_bytes(const std::vector<uint8_t>& v) {
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+}
+
+struct StatusError : std::runtime_error {
+    int code;
+    StatusError(const Status& s) : std::runtime_error(s.msg), code(s.code) {}
+};
+
+void check(const Status& s) {
+    if (!s.ok()) throw StatusError(s);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_rsmi_host, m) {
+    m.doc() = "C++ host layer of the MI355X RS engine (ShardPlugin mirror, Shard codec)";
+    static py::exception<StatusError> exc(m, "HostError");
+    py::register_exception_translator([](std::exception_ptr p) {
+        try {
+            if (p) std::rethrow_exception(p);
+        } catch (const StatusError& e) {
+            PyErr_SetObject(exc.ptr(), py::make_tuple(e.what(), e.code).ptr());
+        }
+    });
+
+    py::class_<Share>(m, "Share")
+        .def(py::init([](int n, const py::bytes& d) { return Share{n, to_vec(d)}; }))
+        .def_readwrite("Number", &Share::Number)
+        .def_property("Data", [](const Share& s) { return to_bytes(s.Data); },
+                      [](Share& s, const py::bytes& b) { s.Data = to_vec(b); })
+        .def("DeepCopy", &Share::DeepCopy);
+
+    py::class_<FEC, std::shared_ptr<FEC>>(m, "FEC")
+        .def("Required", &FEC::Required)
+        .def("Total", &FEC::Total)
+        .def("Encode",
+             [](FEC& f, const py::bytes& input, const std::function<void(Share)>& output) {
+                 const std::string s = input;
+                 check(f.Encode(reinterpret_cast<const uint8_t*>(s.data()), s.size(),
+                                [&](const ShareView& v) { output(v.DeepCopy()); }));
+             })
+        .def("Decode", [](FEC& f, py::object /*dst*/, std::vector<Share>& shares) {
+            std::vector<uint8_t> out;
+            check(f.Decode(&out, shares));
+            return py::make_tuple(to_bytes(out), shares);
+        });
+
+    m.def("NewFEC", [](int k, int n) {
+        std::shared_ptr<FEC> f;
+        check(NewFEC(k, n, &f));
+        return f;
+    });
+
+    py::class_<Shard>(m, "Shard")
+        .def(py::init<>())
+        .def(py::init([](const py::bytes& sig, const py::bytes& data, uint64_t num, uint64_t total,
+                         uint64_t need) {
+                 Shard s;
+                 s.FileSignature = to_vec(sig);
+                 s.ShardData = to_vec(data);
+                 s.ShardNumber = num;
+                 s.TotalShards = total;
+                 s.MinimumNeededShards = need;
+                 return s;
+             }),
+             py::arg("FileSignature") = py::bytes(), py::arg("ShardData") = py::bytes(),
+             py::arg("ShardNumber") = 0, py::arg("TotalShards") = 0,
+             py::arg("MinimumNeededShards") = 0)
+        .def_property("FileSignature", [](const Shard& s) { return to_bytes(s.FileSignature); },
+                      [](Shard& s, const py::bytes& b) { s.FileSignature = to_vec(b); })
+        .def_property("ShardData", [](const Shard& s) { return to_bytes(s.ShardData); },
+                      [](Shard& s, const py::bytes& b) { s.ShardData = to_vec(b); })
+        .def_readwrite("ShardNumber", &Shard::ShardNumber)
+        .def_readwrite("TotalShards", &Shard::TotalShards)
+        .def_readwrite("MinimumNeededShards", &Shard::MinimumNeededShards)
+        .def("Size", &Shard::Size)
+        .def("Marshal", [](const Shard& s) { return to_bytes(s.Marshal()); })
+        .def("Unmarshal",
+             [](Shard& s, const py::bytes& b) {
+                 const std::string d = b;
+                 check(s.Unmarshal(reinterpret_cast<const uint8_t*>(d.data()), d.size()));
+             })
+        .def("__eq__", &Shard::operator==);
+
+    py::class_<PeerID>(m, "PeerID")
+        .def(py::init([](const std::string& addr, const py::bytes& id) { return PeerID{addr, to_vec(id)}; }))
+        .def_readwrite("Address", &PeerID::Address);
+
+    py::class_<ReceiveEvent>(m, "ReceiveEvent")
+        .def_readonly("pooled", &ReceiveEvent::pooled)
+        .def_readonly("decoded", &ReceiveEvent::decoded)
+        .def_readonly("verified", &ReceiveEvent::verified)
+        .def_property_readonly("decode_code", [](const ReceiveEvent& e) { return e.decode_status.code; })
+        .def_property_readonly("message", [](const ReceiveEvent& e) { return to_bytes(e.message); });
+
+    py::class_<ShardPlugin>(m, "ShardPlugin")
+        .def_readwrite("MinimumNeededShards", &ShardPlugin::MinimumNeededShards)
+        .def_readwrite("TotalShards", &ShardPlugin::TotalShards)
+        .def("Receive",
+             [](ShardPlugin& p, const PeerID& sender, const Shard& msg) {
+                 ReceiveEvent ev;
+                 check(p.Receive(sender, msg, &ev));
+                 return ev;
+             })
+        .def("prepareShards",
+             [](ShardPlugin& p, const PeerID& self, py::object input) {
+                 std::vector<Shard> out;
+                 if (input.is_none()) {
+                     check(p.prepareShards(self, nullptr, &out));
+                 } else {
+                     const std::vector<uint8_t> v = to_vec(input.cast<py::bytes>());
+                     check(p.prepareShards(self, &v, &out));
+                 }
+                 return out;
+             })
+        .def("ShardAndBroadcast",
+             [](ShardPlugin& p, const PeerID& self, const py::bytes& input,
+                const std::function<void(Shard)>& broadcast) {
+                 const std::vector<uint8_t> v = to_vec(input);
+                 check(p.ShardAndBroadcast(self, &v, [&](const Shard& s) { broadcast(s); }));
+             })
+        .def("shardInput",
+             [](ShardPlugin& p, const py::bytes& input) {
+                 std::vector<Share> out;
+                 check(p.shardInput(to_vec(input), &out));
+                 return out;
+             })
+        .def("PoolSize", [](const ShardPlugin& p, const py::bytes& sig) { return p.PoolSize(to_vec(sig)); });
+
+    m.def("NewShardPlugin",
+          [](std::function<py::bytes(py::bytes)> sign, std::function<bool(py::bytes, py::bytes)> verify,
+             int k, int n) {
+              Signer s = [sign](const std::vector<uint8_t>& msg) {
+                  py::gil_scoped_acquire g;
+                  return to_vec(sign(to_bytes(msg)));
+              };
+              Verifier v = [verify](const std::vector<uint8_t>& msg, const std::vector<uint8_t>& sig) {
+                  py::gil_scoped_acquire g;
+                  return verify(to_bytes(msg), to_bytes(sig));
+              };
+              return NewShardPlugin(s, v, k, n).release();
+          },
+          py::return_value_policy::take_ownership);
+    m.def("serializeMessage", [](const PeerID& id, const py::bytes& msg) {
+        return to_bytes(serializeMessage(id, to_vec(msg)));
+    });
+    m.def("largestPrimeFactors", &largestPrimeFactors);
+    m.def("StatusText", &StatusText);
+}

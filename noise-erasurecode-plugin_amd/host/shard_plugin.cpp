@@ -1,0 +1,198 @@
+// shard_plugin.cpp -- see shard_plugin.hpp.
+#include "shard_plugin.hpp"
+
+#include <algorithm>
+
+#include "../../include/rsmi.h"
+#include "../../include/rsmi_wire.h"
+
+namespace rsmi_host {
+
+// ---------------------------------------------------------------- Shard ----
+static rs_shard_view view_of(const Shard& s) {
+    rs_shard_view v{};
+    v.file_signature = s.FileSignature.data();
+    v.file_signature_len = s.FileSignature.size();
+    v.shard_data = s.ShardData.data();
+    v.shard_data_len = s.ShardData.size();
+    v.shard_number = s.ShardNumber;
+    v.total_shards = s.TotalShards;
+    v.minimum_needed_shards = s.MinimumNeededShards;
+    return v;
+}
+
+size_t Shard::Size() const {
+    const rs_shard_view v = view_of(*this);
+    return rs_shard_size(&v);
+}
+
+std::vector<uint8_t> Shard::Marshal() const {
+    const rs_shard_view v = view_of(*this);
+    std::vector<uint8_t> out(rs_shard_size(&v));
+    size_t w = 0;
+    rs_shard_marshal(&v, out.data(), out.size(), &w);
+    out.resize(w);
+    return out;
+}
+
+Status Shard::Unmarshal(const uint8_t* data, size_t len) {
+    rs_shard_view v{};
+    const int rc = rs_shard_unmarshal(data, len, &v);
+    if (rc != 0) {
+        const char* what = rc == RS_EWIRE_EOF        ? "unexpected EOF"
+                           : rc == RS_EWIRE_OVERFLOW ? "proto: integer overflow"
+                           : rc == RS_EWIRE_LENGTH   ? "proto: negative length found during unmarshaling"
+                                                     : "proto: Shard: bad wire type or tag";
+        return Status::Err(rc, what);
+    }
+    FileSignature.assign(v.file_signature, v.file_signature + v.file_signature_len);
+    ShardData.assign(v.shard_data, v.shard_data + v.shard_data_len);
+    ShardNumber = v.shard_number;
+    TotalShards = v.total_shards;
+    MinimumNeededShards = v.minimum_needed_shards;
+    return Status::Ok();
+}
+
+// ---------------------------------------------------------------- helpers --
+std::vector<uint8_t> serializeMessage(const PeerID& id, const std::vector<uint8_t>& message) {
+    std::vector<uint8_t> out;
+    out.reserve(8 + id.Address.size() + id.Id.size() + message.size());
+    auto put32 = [&](uint32_t v) {
+        for (int i = 0; i < 4; ++i) out.push_back(static_cast<uint8_t>(v >> (8 * i)));
+    };
+    put32(static_cast<uint32_t>(id.Address.size()));
+    out.insert(out.end(), id.Address.begin(), id.Address.end());
+    put32(static_cast<uint32_t>(id.Id.size()));
+    out.insert(out.end(), id.Id.begin(), id.Id.end());
+    out.insert(out.end(), message.begin(), message.end());
+    return out;
+}
+
+int largestPrimeFactors(int n) {
+    int result = -1;
+    while (n > 0 && n % 2 == 0) {
+        result = 2;
+        n /= 2;
+    }
+    for (int i = 3; i * i <= n; i += 2)
+        while (n % i == 0) {
+            result = std::max(result, i);
+            n /= i;
+        }
+    if (n > 2) result = std::max(result, n);
+    return result;
+}
+
+std::string HexString(const std::vector<uint8_t>& b) {
+    static const char* d = "0123456789abcdef";
+    std::string s(b.size() * 2, '0');
+    for (size_t i = 0; i < b.size(); ++i) {
+        s[2 * i] = d[b[i] >> 4];
+        s[2 * i + 1] = d[b[i] & 15];
+    }
+    return s;
+}
+
+// ----------------------------------------------------------- ShardPlugin ---
+ShardPlugin::ShardPlugin(int k, int n, Signer sign, Verifier verify)
+    : MinimumNeededShards(k), TotalShards(n), sign_(std::move(sign)), verify_(std::move(verify)) {}
+
+std::unique_ptr<ShardPlugin> NewShardPlugin(Signer sign, Verifier verify, int k, int n) {
+    return std::make_unique<ShardPlugin>(k, n, std::move(sign), std::move(verify));
+}
+
+size_t ShardPlugin::PoolSize(const std::vector<uint8_t>& sig) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = shards_.find(HexString(sig));
+    return it == shards_.end() ? 0 : it->second.size();
+}
+
+Status ShardPlugin::shardInput(const std::vector<uint8_t>& input, std::vector<Share>* out) {
+    std::shared_ptr<FEC> f;
+    Status st = CachedFEC(MinimumNeededShards, TotalShards, &f);
+    if (!st.ok()) return st;
+    std::vector<Share> shares(static_cast<size_t>(TotalShards));
+    st = f->Encode(input.data(), input.size(), [&](const ShareView& s) {
+        shares[static_cast<size_t>(s.Number)] = s.DeepCopy();  // main.go:255-258
+    });
+    if (!st.ok()) return st;
+    *out = std::move(shares);
+    return Status::Ok();
+}
+
+Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
+                                  std::vector<Shard>* out) {
+    if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
+    const std::vector<uint8_t> sig = sign_ ? sign_(serializeMessage(self, *input))
+                                           : std::vector<uint8_t>();
+    std::vector<Share> shares;
+    Status st = shardInput(*input, &shares);
+    if (!st.ok()) return st;
+    out->clear();
+    for (Share& s : shares) {
+        Shard m;
+        m.FileSignature = sig;
+        m.ShardData = std::move(s.Data);
+        m.ShardNumber = static_cast<uint64_t>(s.Number);
+        m.TotalShards = static_cast<uint64_t>(TotalShards);
+        m.MinimumNeededShards = static_cast<uint64_t>(MinimumNeededShards);
+        out->push_back(std::move(m));
+    }
+    return Status::Ok();
+}
+
+Status ShardPlugin::ShardAndBroadcast(const PeerID& self, const std::vector<uint8_t>* input,
+                                      const std::function<void(const Shard&)>& broadcast) {
+    std::vector<Shard> shards;
+    Status st = prepareShards(self, input, &shards);
+    if (!st.ok()) return st;
+    for (const Shard& s : shards) broadcast(s);
+    return Status::Ok();
+}
+
+Status ShardPlugin::Receive(const PeerID& sender, const Shard& msg, ReceiveEvent* ev) {
+    ReceiveEvent local;
+    ReceiveEvent& e = ev ? *ev : local;
+    e = ReceiveEvent{};
+    const std::string key = HexString(msg.FileSignature);
+    std::vector<Share> pool;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = shards_.find(key);
+        if (it == shards_.end()) {  // main.go:56-62
+            shards_[key].push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+            e.pooled = true;
+            return Status::Ok();
+        }
+        std::vector<Share>& p = it->second;
+        const int64_t len = static_cast<int64_t>(p.size());
+        if (len < static_cast<int64_t>(msg.MinimumNeededShards)) {  // main.go:65-71
+            p.push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+            e.pooled = true;
+            return Status::Ok();
+        }
+        if (!(len >= static_cast<int64_t>(msg.MinimumNeededShards) &&
+              len <= static_cast<int64_t>(msg.TotalShards)))  // main.go:100-101
+            return Status::Err(RS_EINVAL, "Shards mempool is larger than maximum size");
+        pool = p;  // decode a snapshot outside the lock
+    }
+    // main.go:72-99: k and n come from the message.
+    e.decoded = true;
+    std::shared_ptr<FEC> f;
+    e.decode_status = CachedFEC(static_cast<int>(msg.MinimumNeededShards),
+                                static_cast<int>(msg.TotalShards), &f);
+    if (e.decode_status.ok()) e.decode_status = f->Decode(&e.message, pool);
+    if (!e.decode_status.ok()) e.message.clear();
+    e.verified = e.decode_status.ok() && verify_ &&
+                 verify_(serializeMessage(sender, e.message), msg.FileSignature);
+    if (e.verified) {  // main.go:90-92
+        std::lock_guard<std::mutex> lk(mu_);
+        shards_.erase(key);
+        return Status::Ok();
+    }
+    if (pool.size() == msg.TotalShards)  // main.go:96-98
+        return Status::Err(RS_ESINGULAR, "Could not put together the message due to corruption");
+    return Status::Ok();
+}
+
+}  // namespace rsmi_host

@@ -1,0 +1,111 @@
+// shard_plugin.hpp -- C++ mirror of the reference plugin's shard path
+// (/root/reference/main.go), on top of the engine (infectious.hpp):
+//   ShardPlugin{MinimumNeededShards, TotalShards, Shards}  main.go:43-50
+//   Receive (decode branch)                                main.go:52-107
+//   NewShardPlugin                                         main.go:108-115
+//   ShardAndBroadcast                                      main.go:201-210
+//   prepareShards                                          main.go:211-241
+//   shardInput                                             main.go:243-267
+//   serializeMessage                                       main.go:276-302
+//   largestPrimeFactors (CLI k/n re-derivation)            main.go:303-335
+//   erasurecode.Shard + Marshal/Unmarshal/Size             protobuf/shard.proto:21-27
+// Networking, ed25519/blake2b signing and discovery are out of scope
+// (SURVEY.md §2): signing and verification are caller-supplied callbacks and
+// "broadcast" is a callback receiving each Shard.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "infectious.hpp"
+
+namespace rsmi_host {
+
+// erasurecode.Shard (protobuf/shard.pb.go:29-37).
+struct Shard {
+    std::vector<uint8_t> FileSignature;
+    std::vector<uint8_t> ShardData;
+    uint64_t ShardNumber = 0;
+    uint64_t TotalShards = 0;
+    uint64_t MinimumNeededShards = 0;
+
+    size_t Size() const;                                   // shard.pb.go:355
+    std::vector<uint8_t> Marshal() const;                  // shard.pb.go:209
+    Status Unmarshal(const uint8_t* data, size_t len);     // shard.pb.go:413
+    bool operator==(const Shard& o) const {
+        return FileSignature == o.FileSignature && ShardData == o.ShardData &&
+               ShardNumber == o.ShardNumber && TotalShards == o.TotalShards &&
+               MinimumNeededShards == o.MinimumNeededShards;
+    }
+};
+
+// peer.ID as serializeMessage uses it: Address string + Id bytes.
+struct PeerID {
+    std::string Address;
+    std::vector<uint8_t> Id;
+};
+
+// [u32le len(Address)][Address][u32le len(Id)][Id][message]  (main.go:276-302)
+std::vector<uint8_t> serializeMessage(const PeerID& id, const std::vector<uint8_t>& message);
+
+// main.go:303-335; -1 for n < 2 (the reference's initial value).
+int largestPrimeFactors(int n);
+
+// keys.Sign(policy, hash, msg) stand-in and crypto.Verify stand-in.
+using Signer = std::function<std::vector<uint8_t>(const std::vector<uint8_t>& msg)>;
+using Verifier = std::function<bool(const std::vector<uint8_t>& msg,
+                                    const std::vector<uint8_t>& signature)>;
+
+// What Receive did with one message (the reference only logs it).
+struct ReceiveEvent {
+    bool pooled = false;      // shard appended to / created the mempool
+    bool decoded = false;     // decode branch ran (main.go:72-99)
+    bool verified = false;    // signature check passed; pool deleted
+    Status decode_status;     // NewFEC / Decode error (logged by the reference)
+    std::vector<uint8_t> message;  // completeMessage
+};
+
+class ShardPlugin {
+public:
+    int MinimumNeededShards;
+    int TotalShards;
+
+    ShardPlugin(int minimumNeededShards, int totalShards, Signer sign, Verifier verify);
+
+    // main.go:52-107.  `sender` = ctx.Sender().  The mempool update is done
+    // under one lock (the reference's Load->Delete->Store on sync.Map is not
+    // atomic); the pooling rules are unchanged: shards are
+    // appended until MinimumNeededShards are held, the next shard triggers
+    // the decode of the pool (without itself being added), a pool holding
+    // more than TotalShards is an error.
+    Status Receive(const PeerID& sender, const Shard& msg, ReceiveEvent* ev = nullptr);
+
+    // main.go:201-210 with net.Broadcast replaced by `broadcast`.
+    Status ShardAndBroadcast(const PeerID& self, const std::vector<uint8_t>* input,
+                             const std::function<void(const Shard&)>& broadcast);
+    // main.go:211-241 (input == nullptr -> "network: input is null").
+    Status prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
+                         std::vector<Shard>* out);
+    // main.go:243-267
+    Status shardInput(const std::vector<uint8_t>& input, std::vector<Share>* out);
+
+    size_t PoolSize(const std::vector<uint8_t>& fileSignature) const;
+
+private:
+    Signer sign_;
+    Verifier verify_;
+    mutable std::mutex mu_;
+    std::unordered_map<std::string, std::vector<Share>> shards_;  // key: hex(signature)
+};
+
+// NewShardPlugin(signaturePolicy, hashPolicy, k, n)  main.go:108-115
+std::unique_ptr<ShardPlugin> NewShardPlugin(Signer sign, Verifier verify, int minimumNeededShards,
+                                            int totalShards);
+
+std::string HexString(const std::vector<uint8_t>& b);  // fmt.Sprintf("%x", ...)
+
+}  // namespace rsmi_host

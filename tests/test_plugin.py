@@ -1,0 +1,179 @@
+"""GPU: the C++ ShardPlugin mirror (noise-erasurecode-plugin_amd/host/) on
+the engine, driven like the reference plugin (main.go): prepareShards /
+shardInput on the send side, Receive pooling + decode on the receive side,
+the Shard wire format in between, checked against the oracle.
+
+Signing is out of scope: the tests sign with a 64-byte
+SHA-512 digest of serializeMessage(...) as a stand-in for ed25519/blake2b,
+and verify by recomputing it.
+"""
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from oracle import oracle  # noqa: E402
+from rsmi import host as h  # noqa: E402
+
+SELF = h.PeerID("tcp://localhost:3000", b"\x11" * 32)
+
+
+def sign(msg):
+    return hashlib.sha512(msg).digest()
+
+
+def verify(msg, sig):
+    return hashlib.sha512(msg).digest() == sig
+
+
+def plugin(k, n):
+    return h.NewShardPlugin(sign, verify, k, n)
+
+
+def test_prepare_shards_layout_and_parity():
+    k, n = 4, 6  # plugin defaults, main.go:34-35
+    p = plugin(k, n)
+    msg = b"hello, world! __" * 4  # 64 bytes, multiple of k
+    shards = p.prepareShards(SELF, msg)
+    assert len(shards) == n
+    S = len(msg) // k
+    sig = sign(h.serializeMessage(SELF, msg))
+    par = oracle.encode(oracle.fec_matrix(k, n), k, n, msg)
+    for i, s in enumerate(shards):
+        assert s.FileSignature == sig
+        assert (s.ShardNumber, s.TotalShards, s.MinimumNeededShards) == (i, n, k)
+        want = msg[i * S:(i + 1) * S] if i < k else par[(i - k) * S:(i - k + 1) * S]
+        assert s.ShardData == want
+    with pytest.raises(h.HostError):
+        p.prepareShards(SELF, None)  # main.go:215 "network: input is null"
+    with pytest.raises(h.HostError):
+        p.prepareShards(SELF, b"abc")  # len % k != 0: Encode error
+
+
+def test_receive_pooling_rules():
+    k, n = 4, 6
+    sender = h.PeerID("tcp://peer:3001", b"\x22" * 32)
+    p = plugin(k, n)
+    msg = bytes(range(40))
+    shards = p.prepareShards(sender, msg)
+    order = [5, 0, 3, 4, 1, 2]
+    evs = []
+    for i in order:
+        wire = shards[i].Marshal()
+        s = h.Shard()
+        s.Unmarshal(wire)
+        evs.append(p.Receive(sender, s))
+    # first k arrivals are pooled, the (k+1)-th triggers the decode of the pool
+    # without being added (main.go:65-72); verification deletes the pool.
+    assert [e.pooled for e in evs[:k]] == [True] * k
+    assert evs[k].decoded and evs[k].verified and evs[k].message == msg
+    # the pool was deleted on success, so the late sixth shard starts a new one
+    assert evs[k + 1].pooled and p.PoolSize(shards[0].FileSignature) == 1
+
+
+def test_receive_corrupted_and_duplicate_shards():
+    k, n = 4, 6
+    p = plugin(k, n)
+    msg = bytes(range(100, 140))
+    shards = p.prepareShards(SELF, msg)
+    bad = h.Shard(shards[1].FileSignature, bytes(len(shards[1].ShardData)), 1, n, k)
+    for s in (shards[0], bad, shards[2], shards[4]):
+        p.Receive(SELF, s)
+    ev = p.Receive(SELF, shards[5])
+    assert ev.decoded and not ev.verified  # "malformed signature", pool kept
+    assert p.PoolSize(shards[0].FileSignature) == k
+    # duplicate numbers: Decode fails (fewer than k distinct shares)
+    p2 = plugin(k, n)
+    for s in (shards[0], shards[0], shards[2], shards[3]):
+        p2.Receive(SELF, s)
+    ev = p2.Receive(SELF, shards[4])
+    assert ev.decoded and not ev.verified and ev.decode_code != 0
+
+
+def test_receive_pool_overflow_error():
+    # k from the message larger than the pool bound n -> error branch (main.go:100-101)
+    p = plugin(4, 6)
+    sig = b"\x33" * 64
+    for i in range(3):
+        p.Receive(SELF, h.Shard(sig, b"ab", i, 6, 3))
+    with pytest.raises(h.HostError):
+        p.Receive(SELF, h.Shard(sig, b"ab", 3, 2, 3))  # pool 3 > TotalShards 2
+
+
+def test_all_drop_patterns_rs10_4_through_wire():
+    """Receive decodes on the (k+1)-th arrival (k pooled + the trigger, which
+    is not added: main.go:65-77), so the plugin reconstructs with up to m-1
+    lost shards; with exactly m lost only k shards ever arrive and Receive
+    never decodes -- a property of the reference, mirrored.  Those cases are
+    decoded from the pooled shares with FEC.Decode (what config 1 times)."""
+    k, n = 10, 14
+    p = plugin(k, n)
+    msg = oracle.splitmix_bytes(10 * 37, 3).tobytes()
+    shards = [x.Marshal() for x in p.prepareShards(SELF, msg)]
+    f = h.NewFEC(k, n)
+    for e in range(0, 5):
+        for lost in itertools.combinations(range(n), e):
+            keep = [i for i in range(n) if i not in lost]
+            recv = plugin(k, n)
+            evs = []
+            got = []
+            for i in keep[:k + 1]:
+                s = h.Shard()
+                s.Unmarshal(shards[i])
+                got.append(h.Share(int(s.ShardNumber), s.ShardData))
+                evs.append(recv.Receive(SELF, s))
+            if e < n - k:
+                assert evs[-1].decoded and evs[-1].verified and evs[-1].message == msg, lost
+            else:
+                assert not any(ev.decoded for ev in evs)
+                assert recv.PoolSize(s.FileSignature) == k
+                assert f.Decode(None, got[:k])[0] == msg, lost
+
+
+def test_config1_blob_rs10_4():
+    """BASELINE config 1: a 1 MiB blob (zero-padded to 1,048,580 B) encoded
+    into 14 protobuf Shards, 4 dropped (seeded), the rest received and
+    reconstructed; bit-exact vs the oracle on both sides."""
+    k, n = 10, 14
+    blob = oracle.splitmix_bytes(1 << 20, 0x5EED).tobytes() + b"\0" * 4
+    p = plugin(k, n)
+    shards = p.prepareShards(SELF, blob)
+    par = oracle.encode(oracle.fec_matrix(k, n), k, n, blob)
+    S = len(blob) // k
+    assert b"".join(s.ShardData for s in shards[k:]) == par
+    wires = [s.Marshal() for s in shards]
+    assert wires[0][66:70] == bytes([0x12, 0x9A, 0xB3, 0x06])  # tag 2, len 104,858 varint
+    rng = np.random.default_rng(0xE4A5)
+    lost = set(rng.choice(n, size=4, replace=False).tolist())
+    recv = plugin(k, n)
+    shares = []
+    for i in [i for i in range(n) if i not in lost]:
+        s = h.Shard()
+        s.Unmarshal(wires[i])
+        recv.Receive(SELF, s)
+        shares.append(h.Share(int(s.ShardNumber), s.ShardData))
+    # 4 lost = m: the pool holds k shares and Receive waits for a trigger
+    # shard that never comes; decode the pooled shares directly.
+    got, _ = h.NewFEC(k, n).Decode(None, shares[::-1])
+    assert got == blob
+
+
+def test_host_fec_api():
+    f = h.NewFEC(8, 14)
+    assert (f.Required(), f.Total()) == (8, 14)
+    shares = []
+    f.Encode(b"hello, world! __", lambda s: shares.append(s.DeepCopy()))
+    assert [s.Number for s in shares] == list(range(14))
+    assert [s.Data for s in shares[:8]] == [b"he", b"ll", b"o,", b" w", b"or", b"ld", b"! ", b"__"]
+    par = oracle.encode(oracle.fec_matrix(8, 14), 8, 14, b"hello, world! __")
+    assert b"".join(s.Data for s in shares[8:]) == par
+    got, sorted_shares = f.Decode(None, [shares[i] for i in (13, 1, 9, 2, 12, 3, 11, 7)])
+    assert got == b"hello, world! __"
+    assert [s.Number for s in sorted_shares] == sorted([13, 1, 9, 2, 12, 3, 11, 7])
