@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--emin", type=int, default=1)
     ap.add_argument("--emax", type=int, default=None)
     ap.add_argument("--mode", choices=["both", "encode", "reconstruct"], default="both")
+    ap.add_argument("--pattern-pool", type=int, default=-1,
+                    help="draw per-stripe erasures from this many distinct patterns "
+                         "(-1: auto = unbounded when all <= emax patterns can be precomputed, "
+                         "else 256)")
     ap.add_argument("--erase", default=None,
                     help="fixed erased shard ids for every stripe, e.g. 0,1,2,3 (default random)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -59,15 +63,25 @@ def parse():
     return ap.parse_args()
 
 
-def erasure_sets(rng, count, stripes, n, emin, emax):
-    out = []
-    for _ in range(count):
-        er = np.zeros((stripes, n), dtype=np.uint8)
-        es = rng.integers(emin, emax + 1, size=stripes)
-        for s in range(stripes):
+def erasure_sets(rng, count, stripes, n, emin, emax, pool=0):
+    """`count` arrays of per-stripe erasure flags: e uniform in [emin, emax],
+    positions uniform without replacement; with pool > 0 every stripe takes
+    one of `pool` such patterns (drawn once)."""
+    def draw(rows):
+        er = np.zeros((rows, n), dtype=np.uint8)
+        es = rng.integers(emin, emax + 1, size=rows)
+        for s in range(rows):
             er[s, rng.choice(n, size=int(es[s]), replace=False)] = 1
-        out.append(er)
-    return out
+        return er
+    if pool > 0:
+        pats = draw(pool)
+        return [pats[rng.integers(0, pool, size=stripes)] for _ in range(count)]
+    return [draw(stripes) for _ in range(count)]
+
+
+def pattern_total(n, emax):
+    from math import comb
+    return sum(comb(n, e) for e in range(1, emax + 1))
 
 
 def cpu_baseline(k, n, S, seconds, threads):
@@ -136,14 +150,18 @@ def main():
     parity = torch.empty(stripes * m * S, dtype=torch.uint8, device=dev)
     f.fill_splitmix(data.data_ptr(), data.numel(), 0x5EED ^ (rank << 32), sh)
     f.fill_splitmix(parity.data_ptr(), parity.numel(), 1, sh)
-    f.prepare_patterns(emax, sh)
+    pool = args.pattern_pool
+    if pool < 0:
+        pool = 0 if pattern_total(n, emax) <= (1 << 20) else 256
+    if pattern_total(n, emax) <= (1 << 20):
+        f.prepare_patterns(emax, sh)  # every pattern inverted + uploaded up front
     rng = np.random.default_rng(0xE4A5 + rank)
     if args.erase:
         fixed = np.zeros((stripes, n), dtype=np.uint8)
         fixed[:, [int(v) for v in args.erase.split(",")]] = 1
         ersets = [fixed] * (args.warmup + args.steps)
     else:
-        ersets = erasure_sets(rng, args.warmup + args.steps, stripes, n, args.emin, emax)
+        ersets = erasure_sets(rng, args.warmup + args.steps, stripes, n, args.emin, emax, pool)
     rec_bytes = [int(((k + er.sum(axis=1)) * S).sum()) for er in ersets]
     enc_bytes = stripes * (k + m) * S
 
@@ -235,6 +253,7 @@ def main():
                 "k": k, "n": n, "shard_bytes": S, "stripes_per_gpu": stripes,
                 "data_bytes_per_gpu": stripes * k * S,
                 "parallelism": f"stripe-partitioned x{world}, no collective",
+                "erasure_patterns": "all" if pool == 0 else f"pool of {pool}",
                 "mode": args.mode,
             },
             "breakdown": {

@@ -148,10 +148,13 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
     const uint32_t grp = static_cast<uint32_t>(b % a.groups);
     b /= a.groups;
     const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);
-    const uint64_t s = b / a.chunks;
-    // Stripe word = pattern id << 8 | outputs (one dependent load); encode
-    // (no stripe table) is pattern 0 with all m parity rows.
-    const uint32_t sw = __builtin_amdgcn_readfirstlane(a.stripe_pat ? a.stripe_pat[s] : a.m);
+    const uint64_t sv = b / a.chunks;
+    // Stripe descriptor = {stripe, pattern id << 8 | outputs} (one dependent
+    // load); encode (no table) is stripe sv, pattern 0, all m parity rows.
+    uint2 desc = make_uint2(static_cast<uint32_t>(sv), a.m);
+    if (a.stripe_desc) desc = a.stripe_desc[sv];
+    const uint64_t s = __builtin_amdgcn_readfirstlane(desc.x);
+    const uint32_t sw = __builtin_amdgcn_readfirstlane(desc.y);
     const uint32_t pat = sw >> 8;
     const int e = static_cast<int>(sw & 0xFFu);
     const int row0 = static_cast<int>(grp) * MG;

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -111,7 +112,8 @@ struct rs_ctx {
     size_t uploaded = 0;  // patterns present on the device
     DevBuf d_stripe_pat;
     Staging st_pat;      // pattern-table uploads
-    Staging st_stripe;   // stripe->pattern ids
+    Staging st_stripe;   // stripe descriptors
+    std::vector<uint32_t> scratch_pid, scratch_start;
 
     // Host-buffer API workspaces.
     DevBuf d_work;
@@ -128,16 +130,16 @@ int hip_status(hipError_t e) { return e == hipSuccess ? RS_OK : RS_EDEVICE; }
 size_t dst_stride(const rs_ctx* c) { return std::max<size_t>(16, round_up(c->m, 16)); }
 
 // Device blob of npat patterns: coef bytes [npat][m][k] (padded to 16) |
-// src u32 [npat][k] | dst u32 [npat][dst_stride] | sw u32 [npat], where
-// sw[p] = p << 8 | outputs is the stripe word of a stripe using pattern p.
+// src u32 [npat][k] | dst u32 [npat][dst_stride] | sw u32x2 [npat], where
+// sw[p] = {0, p << 8 | outputs} is the descriptor of stripe 0 using pattern p.
 struct PatLayout {
     size_t coef, src, dst, sw, total;
     PatLayout(const rs_ctx* c, size_t npat) {
         coef = 0;
         src = round_up(npat * c->m * c->k, 16);
         dst = src + npat * c->k * 4;
-        sw = dst + npat * dst_stride(c) * 4;
-        total = sw + npat * 4;
+        sw = round_up(dst + npat * dst_stride(c) * 4, 8);
+        total = sw + npat * 8;
     }
 };
 
@@ -150,8 +152,8 @@ void pack_patterns(const rs_ctx* c, size_t npat, const uint8_t* coef, const uint
     std::memcpy(out + L.src, src, npat * c->k * 4);
     for (size_t p = 0; p < npat; ++p) {
         std::memcpy(out + L.dst + p * ds * 4, dst + p * c->m, c->m * 4);
-        const uint32_t sw = static_cast<uint32_t>(p << 8) | cnt[p];
-        std::memcpy(out + L.sw + p * 4, &sw, 4);
+        const uint32_t desc[2] = {0u, static_cast<uint32_t>(p << 8) | cnt[p]};
+        std::memcpy(out + L.sw + p * 8, desc, 8);
     }
 }
 
@@ -162,12 +164,13 @@ void set_patterns(const rs_ctx* c, size_t npat, const void* dev, rsmi::MatArgs& 
     a.src = reinterpret_cast<const uint32_t*>(b + L.src);
     a.dst = reinterpret_cast<const uint32_t*>(b + L.dst);
     a.dst_stride = static_cast<uint32_t>(dst_stride(c));
-    a.stripe_pat = nullptr;
+    a.stripe_desc = nullptr;
 }
 
-// Stripe word of pattern 0 of a blob (single-stripe launches with e < m).
-const uint32_t* first_stripe_word(const rs_ctx* c, const void* dev) {
-    return reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(dev) + PatLayout(c, 1).sw);
+// Descriptor {stripe 0, sw[0]} of a one-pattern blob (single-stripe launches
+// with e < m outputs): the blob's sw section holds {0, p << 8 | cnt} pairs.
+const uint2* first_stripe_desc(const rs_ctx* c, const void* dev) {
+    return reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(dev) + PatLayout(c, 1).sw);
 }
 
 bool check_stripes_args(const rs_ctx* c, const void* data, size_t dss, const void* parity,
@@ -214,15 +217,6 @@ int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
         *err = RS_ENOT_ENOUGH;
         return -1;
     }
-    if (c->pat_index.size() >= (size_t(1) << 20)) {  // bound the cache (ids are 24-bit): start over
-        (void)hipDeviceSynchronize();
-        c->pat_index.clear();
-        c->h_coef.clear();
-        c->h_src.clear();
-        c->h_dst.clear();
-        c->h_cnt.clear();
-        c->uploaded = 0;
-    }
     std::vector<int> surv = rsmi::choose_survivors(present.data(), c->k, c->n);
     std::vector<uint8_t> rows;
     if (!targets.empty() && !rsmi::decode_rows(c->enc, c->k, c->n, surv, targets, rows)) {
@@ -239,6 +233,17 @@ int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
     c->h_cnt.push_back(static_cast<uint32_t>(targets.size()));
     c->pat_index.emplace(std::move(key), id);
     return id;
+}
+
+// Drops the decode-pattern cache (bounded: pattern ids are 24 bits).
+void reset_patterns(rs_ctx* c) {
+    (void)hipDeviceSynchronize();
+    c->pat_index.clear();
+    c->h_coef.clear();
+    c->h_src.clear();
+    c->h_dst.clear();
+    c->h_cnt.clear();
+    c->uploaded = 0;
 }
 
 int upload_patterns(rs_ctx* c, hipStream_t s) {
@@ -396,7 +401,7 @@ int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, siz
     if (!g.ok) return RS_EDEVICE;
     rsmi::MatArgs a = base_args(c, const_cast<void*>(data), dss, parity, pss, pitch, len, stripes);
     set_patterns(c, 1, c->d_encpat.p, a);
-    a.stripe_pat = nullptr;
+    a.stripe_desc = nullptr;
     return hip_status(rsmi::launch_matmul(a, c->m, static_cast<hipStream_t>(stream)));
 }
 
@@ -410,27 +415,47 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!c->st_stripe.acquire(stripes * sizeof(uint32_t))) return RS_ENOMEM;
-    uint32_t* ids = static_cast<uint32_t*>(c->st_stripe.p);
+    if (c->pat_index.size() + stripes > (size_t(1) << 20)) reset_patterns(c);  // ids are 24-bit
+    // Pattern of every stripe, then a counting sort by pattern: the launch
+    // lists stripes grouped by pattern (see rs_kernels.hpp stripe_desc).
+    std::vector<uint32_t>& pid = c->scratch_pid;
+    pid.resize(stripes);
     int max_e = 0;
     for (size_t i = 0; i < stripes; ++i) {
         int err = RS_OK;
-        int id = pattern_for(c, erased + i * c->n, &err);
+        const int id = pattern_for(c, erased + i * c->n, &err);
         if (id < 0) return err;
-        ids[i] = (static_cast<uint32_t>(id) << 8) | c->h_cnt[id];
-        max_e = std::max<int>(max_e, c->h_cnt[id]);
+        pid[i] = static_cast<uint32_t>(id);
+        max_e = std::max<int>(max_e, static_cast<int>(c->h_cnt[id]));
     }
     if (max_e == 0) return RS_OK;  // nothing erased anywhere
+    // Counting sort of the stripes by pattern (bucket = pattern id; the
+    // RSMI_NO_SORT knob keeps address order for A/B runs).
+    static const bool no_sort = std::getenv("RSMI_NO_SORT") != nullptr;
+    const size_t nb = no_sort ? 1 : c->h_cnt.size();
+    auto bucket = [&](size_t i) -> size_t { return no_sort ? 0 : pid[i]; };
+    std::vector<uint32_t>& start = c->scratch_start;
+    start.assign(nb + 1, 0);
+    for (size_t i = 0; i < stripes; ++i)
+        if (c->h_cnt[pid[i]]) ++start[bucket(i) + 1];  // stripes with nothing erased are skipped
+    for (size_t b = 0; b < nb; ++b) start[b + 1] += start[b];
+    const size_t used = start[nb];
+    if (!c->st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
+    uint2* desc = static_cast<uint2*>(c->st_stripe.p);
+    for (size_t i = 0; i < stripes; ++i) {
+        const uint32_t p = pid[i];
+        if (c->h_cnt[p]) desc[start[bucket(i)]++] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
+    }
     int st = upload_patterns(c, s);
     if (st != RS_OK) return st;
-    if (!c->d_stripe_pat.reserve(stripes * sizeof(uint32_t))) return RS_ENOMEM;
-    hipError_t e = hipMemcpyAsync(c->d_stripe_pat.p, ids, stripes * sizeof(uint32_t),
+    if (!c->d_stripe_pat.reserve(used * sizeof(uint2))) return RS_ENOMEM;
+    hipError_t e = hipMemcpyAsync(c->d_stripe_pat.p, desc, used * sizeof(uint2),
                                   hipMemcpyHostToDevice, s);
     c->st_stripe.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
-    rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, stripes);
+    rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used);
     set_patterns(c, c->h_cnt.size(), c->d_pats.p, a);
-    a.stripe_pat = static_cast<const uint32_t*>(c->d_stripe_pat.p);
+    a.stripe_desc = static_cast<const uint2*>(c->d_stripe_pat.p);
     return hip_status(rsmi::launch_matmul(a, max_e, s));
 }
 
@@ -532,7 +557,7 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (err != hipSuccess) return RS_EDEVICE;
     rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, share_len, 1);
     set_patterns(c, 1, c->d_onepat.p, a);
-    a.stripe_pat = first_stripe_word(c, c->d_onepat.p);  // e outputs, not m
+    a.stripe_desc = first_stripe_desc(c, c->d_onepat.p);  // e outputs, not m
     err = rsmi::launch_matmul(a, e, s);
     for (int t = 0; t < e && err == hipSuccess; ++t)
         err = hipMemcpyAsync(dst + static_cast<size_t>(missing[t]) * share_len, dout + pitch * t,

@@ -279,3 +279,25 @@ def test_full_size_rs10_4_roundtrip():
     f.sync()
     assert torch.equal(data, d0)
     assert torch.equal(parity, p0)
+
+
+def test_distributed_owner_buffer_reconstruct_world1():
+    """rsmi.distributed with G = 1: the owner buffer [owned, n, S] layout
+    reconstructs in place through rs_reconstruct_stripes (the RCCL exchange
+    itself is covered by tests/test_distributed.py with gloo)."""
+    from rsmi import distributed as rd
+    k, n, S, stripes = 10, 14, 4096, 9
+    f = fec(k, n)
+    data, parity = _dev_stripes(f, stripes, S, S, 31)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), (n - k) * S, S, S, stripes)
+    f.sync()
+    full = torch.cat([data.view(stripes, k, S), parity.view(stripes, n - k, S)], dim=1).contiguous()
+    er = _erasures(np.random.default_rng(9), stripes, n, n - k)
+    plan = rd.plan_exchange(er, k, n, 0, 1, S)
+    held = full.clone()
+    out = rd.gather_survivors(held, plan, n) if False else held  # G = 1: all local
+    bad = torch.from_numpy(er.astype(bool)).cuda()
+    out[bad] = 0
+    rd.reconstruct_owned(f, out, er)
+    f.sync()
+    assert torch.equal(out, full)
