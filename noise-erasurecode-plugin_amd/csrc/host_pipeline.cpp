@@ -1,0 +1,184 @@
+// host_pipeline.cpp -- see host_pipeline.hpp.
+#include "host_pipeline.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+namespace rsmi {
+
+namespace {
+constexpr size_t kPart = size_t(1) << 20;          // memcpy split granularity
+constexpr size_t kChunkBytes = size_t(8) << 20;    // survivor bytes staged per chunk
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int pool_threads() {
+    const char* e = std::getenv("RSMI_COPY_THREADS");
+    int t = e ? std::atoi(e) : static_cast<int>(std::thread::hardware_concurrency());
+    return std::max(1, std::min(t, 8));
+}
+}  // namespace
+
+// ------------------------------------------------------------ CopyPool ----
+CopyPool::CopyPool(int threads) {
+    for (int i = 0; i < threads - 1; ++i) threads_.emplace_back([this] { worker(); });
+}
+
+CopyPool::~CopyPool() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : threads_) t.join();
+}
+
+void CopyPool::worker() {
+    size_t seen = 0;
+    for (;;) {
+        Piece p{};
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return stop_ || (generation_ != seen && next_ < work_.size()); });
+            if (stop_) return;
+            p = work_[next_++];
+            if (next_ == work_.size()) seen = generation_;
+        }
+        std::memcpy(p.dst, p.src, p.len);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (++finished_ == work_.size()) done_cv_.notify_all();
+        }
+    }
+}
+
+void CopyPool::run(const std::vector<Piece>& pieces) {
+    std::vector<Piece> parts;
+    for (const Piece& p : pieces)
+        for (size_t o = 0; o < p.len; o += kPart)
+            parts.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o,
+                             std::min(kPart, p.len - o)});
+    if (parts.empty()) return;
+    if (threads_.empty() || parts.size() == 1) {
+        for (const Piece& p : parts) std::memcpy(p.dst, p.src, p.len);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        work_ = std::move(parts);
+        next_ = 0;
+        finished_ = 0;
+        ++generation_;
+    }
+    cv_.notify_all();
+    // the calling thread helps
+    for (;;) {
+        Piece p{};
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (next_ >= work_.size()) break;
+            p = work_[next_++];
+        }
+        std::memcpy(p.dst, p.src, p.len);
+        std::lock_guard<std::mutex> lk(mu_);
+        if (++finished_ == work_.size()) done_cv_.notify_all();
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return finished_ == work_.size(); });
+}
+
+// -------------------------------------------------------- HostPipeline ----
+HostPipeline::HostPipeline() : pool_(pool_threads()) {}
+
+HostPipeline::~HostPipeline() {
+    for (Slot& s : slots_) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_in) (void)hipFree(s.d_in);
+        if (s.d_out) (void)hipFree(s.d_out);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+}
+
+bool HostPipeline::ensure(Slot& s, size_t in_bytes, size_t out_bytes) {
+    if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return false;
+    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return false;
+    if (in_bytes > s.cap_in) {
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.d_in) (void)hipFree(s.d_in);
+        s.h_in = s.d_in = nullptr;
+        s.cap_in = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_in), in_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.d_in), in_bytes) != hipSuccess)
+            return false;
+        s.cap_in = in_bytes;
+    }
+    if (out_bytes > s.cap_out) {
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_out) (void)hipFree(s.d_out);
+        s.h_out = s.d_out = nullptr;
+        s.cap_out = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_out), out_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&s.d_out), out_bytes) != hipSuccess)
+            return false;
+        s.cap_out = out_bytes;
+    }
+    return true;
+}
+
+hipError_t HostPipeline::drain(Slot& s, uint8_t* const* dsts, int e) {
+    if (!s.pending) return hipSuccess;
+    s.pending = false;
+    const hipError_t err = hipEventSynchronize(s.done);
+    if (err != hipSuccess) return err;
+    std::vector<CopyPool::Piece> out;
+    for (int t = 0; t < e; ++t) out.push_back({dsts[t] + s.c0, s.h_out + t * s.pitch, s.w});
+    pool_.run(out);
+    return hipSuccess;
+}
+
+hipError_t HostPipeline::run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e,
+                             size_t S, const ChunkLaunch& launch) {
+    if (S == 0 || e == 0) return hipSuccess;
+    // Column chunk per shard: about kChunkBytes of survivors per chunk.
+    const size_t cb = round_up(std::min(S, std::max<size_t>(4096, kChunkBytes / k)), 256);
+    const size_t nchunks = (S + cb - 1) / cb;
+    hipError_t err = hipSuccess;
+    size_t c = 0;
+    for (; c < nchunks && err == hipSuccess; ++c) {
+        Slot& s = slots_[c % kSlots];
+        err = drain(s, dsts, e);  // results of chunk c - kSlots
+        if (err != hipSuccess) break;
+        if (!ensure(s, cb * static_cast<size_t>(k), cb * static_cast<size_t>(e))) {
+            err = hipErrorOutOfMemory;
+            break;
+        }
+        const size_t c0 = c * cb, w = std::min(cb, S - c0);
+        std::vector<CopyPool::Piece> in;
+        for (int j = 0; j < k; ++j) in.push_back({s.h_in + j * cb, srcs[j] + c0, w});
+        pool_.run(in);
+        err = hipMemcpyAsync(s.d_in, s.h_in, cb * static_cast<size_t>(k), hipMemcpyHostToDevice, s.stream);
+        if (err == hipSuccess) err = launch(s.d_in, s.d_out, cb, w, s.stream);
+        if (err == hipSuccess)
+            err = hipMemcpyAsync(s.h_out, s.d_out, cb * static_cast<size_t>(e), hipMemcpyDeviceToHost, s.stream);
+        if (err == hipSuccess) err = hipEventRecord(s.done, s.stream);
+        if (err == hipSuccess) {
+            s.pending = true;
+            s.c0 = c0;
+            s.w = w;
+            s.pitch = cb;
+        }
+    }
+    // Drain the last chunks in order (also after an error, so no slot is
+    // left holding a pending copy into caller memory).
+    for (size_t i = 0; i < kSlots; ++i) {
+        Slot& s = slots_[(c + i) % kSlots];
+        const hipError_t d = drain(s, dsts, e);
+        if (err == hipSuccess) err = d;
+    }
+    return err;
+}
+
+}  // namespace rsmi

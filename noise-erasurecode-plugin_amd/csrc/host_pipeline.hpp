@@ -1,0 +1,76 @@
+// host_pipeline.hpp -- the host-buffer path of the C ABI (rs_encode /
+// rs_decode, i.e. the cgo calls replacing infectious Encode/Decode at
+// main.go:262 / :77): caller bytes are streamed through pinned
+// (hipHostMalloc) staging in column chunks, with each chunk's H2D copy,
+// kernel and D2H copy on one of three HIP streams so that chunk c's GPU work
+// overlaps the staging copies of chunks c-1 and c+1.  Pageable <-> pinned
+// copies are split over a small worker pool.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace rsmi {
+
+// Fixed set of worker threads running memcpy pieces.
+class CopyPool {
+public:
+    explicit CopyPool(int threads);
+    ~CopyPool();
+    struct Piece {
+        void* dst;
+        const void* src;
+        size_t len;
+    };
+    // Copies every piece (split further into <= 1 MiB parts); returns when done.
+    void run(const std::vector<Piece>& pieces);
+
+private:
+    void worker();
+    std::vector<std::thread> threads_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<Piece> work_;
+    size_t next_ = 0, finished_ = 0, generation_ = 0;
+    bool stop_ = false;
+};
+
+// Launches the GF kernel for one chunk: survivors at din + j*pitch (j < k),
+// outputs at dout + t*pitch, w coded bytes per shard.
+using ChunkLaunch = std::function<hipError_t(uint8_t* din, uint8_t* dout, size_t pitch,
+                                             size_t w, hipStream_t stream)>;
+
+class HostPipeline {
+public:
+    HostPipeline();
+    ~HostPipeline();
+    // out_t[0..S) = f(srcs[0..k)[0..S)) for t < e, streamed in chunks.
+    hipError_t run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e, size_t S,
+                   const ChunkLaunch& launch);
+
+    static constexpr int kSlots = 3;
+
+private:
+    struct Slot {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+        size_t cap_in = 0, cap_out = 0;
+        bool pending = false;
+        size_t c0 = 0, w = 0, pitch = 0;
+    };
+    bool ensure(Slot& s, size_t in_bytes, size_t out_bytes);
+    hipError_t drain(Slot& s, uint8_t* const* dsts, int e);
+    Slot slots_[kSlots];
+    CopyPool pool_;
+};
+
+}  // namespace rsmi

@@ -133,8 +133,8 @@ __device__ __forceinline__ void step_fence(uint32_t (&acc)[kRowsPerStep][4]) {
 
 // One block codes a chunk of 16-byte columns of one stripe for one group of
 // MG output rows.  LDS: [k][MG/4][20] table dwords | k survivor pointers.
-template <int K, int MG>
-__global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
+template <int K, int MG, int BT>
+__global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     static_assert(MG % kRowsPerStep == 0, "MG must be a multiple of 4");
     constexpr int TG = MG / kRowsPerStep;                 // sub-steps per survivor
     constexpr bool kRegPtrs = K > 0 && K <= 16;           // survivor bases kept in SGPRs
@@ -164,8 +164,8 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
     // This lane's coefficient byte for the table build is requested first, so
     // waiting for it later does not wait for the survivor loads behind it.
     const uint8_t* coef = a.coef + (static_cast<size_t>(pat) * a.m + row0) * k;
-    uint32_t cbyte[(K > 0 && K * MG <= kBlock) ? 1 : 1];
-    const bool one_coef = (K > 0 && K * MG <= kBlock);
+    uint32_t cbyte[(K > 0 && K * MG <= BT) ? 1 : 1];
+    const bool one_coef = (K > 0 && K * MG <= BT);
     if (one_coef) {
         const int j = threadIdx.x / MG, t = threadIdx.x - j * MG;
         cbyte[0] = (static_cast<int>(threadIdx.x) < k * MG && t < eg) ? coef[t * k + j] : 0u;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
 #pragma unroll
         for (int j = 0; j < K; ++j) sp[j] = uniform_ptr(shard(__builtin_amdgcn_readfirstlane(srcid[j])));
     } else {
-        for (int i = threadIdx.x; i < k; i += kBlock) sptr[i] = shard(srcid[i]);
+        for (int i = threadIdx.x; i < k; i += BT) sptr[i] = shard(srcid[i]);
     }
     const uint32_t last = a.ncols16 - 1;
     // Survivor loads of the block's first iteration are issued before the
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
     // their HBM latency; with one iteration per block (the default) this is
     // the whole data path.
     uint4 xpre[kRegPtrs ? K : 1];
-    const uint32_t col0 = chunk * a.iters * kBlock + threadIdx.x;
+    const uint32_t col0 = chunk * a.iters * BT + threadIdx.x;
     const uint32_t off0 = (col0 <= last ? col0 : last) * 16u;
     if constexpr (kRegPtrs) {
 #pragma unroll
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
             build_tables(cbyte[0], &tw[(j * TG + t / kRowsPerStep) * kStepWords + (t % kRowsPerStep) * 5]);
         }
     } else {
-        for (int idx = threadIdx.x; idx < k * MG; idx += kBlock) {
+        for (int idx = threadIdx.x; idx < k * MG; idx += BT) {
             const int j = idx / MG, t = idx - j * MG;
             const uint32_t c = (t < eg) ? coef[t * k + j] : 0u;
             build_tables(c, &tw[(j * TG + t / kRowsPerStep) * kStepWords + (t % kRowsPerStep) * 5]);
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
     __syncthreads();
 
     for (uint32_t it = 0; it < a.iters; ++it) {
-        const uint32_t colbase = (chunk * a.iters + it) * kBlock;
+        const uint32_t colbase = (chunk * a.iters + it) * BT;
         if (colbase >= a.ncols16) break;
         RS_MEM_FENCE();
         const uint32_t col = colbase + threadIdx.x;
@@ -274,8 +274,8 @@ __global__ __launch_bounds__(kBlock) void rs_matmul_kernel(MatArgs a) {
         if constexpr (kRegPtrs) {
             // Software pipelining: the next iteration's survivor loads go out
             // before this iteration's stores.
-            const uint32_t ncol = colbase + kBlock + threadIdx.x;
-            if (it + 1 < a.iters && colbase + kBlock < a.ncols16) {
+            const uint32_t ncol = colbase + BT + threadIdx.x;
+            if (it + 1 < a.iters && colbase + BT < a.ncols16) {
                 const uint32_t noff = (ncol <= last ? ncol : last) * 16u;
 #pragma unroll
                 for (int j = 0; j < K; ++j) xpre[j] = gload16(sp[j] + noff);
@@ -310,25 +310,33 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint8_t* p, size_
 }
 
 struct Variant {
-    int K, MG;
+    int K, MG, BT;
     const char* name;
     void (*fn)(MatArgs);
 };
 
-#define RS_VARIANT(K, MG) {K, MG, "K" #K "_MG" #MG, rs_matmul_kernel<K, MG>}
+#define RS_VARIANT(K, MG, BT) {K, MG, BT, "K" #K "_MG" #MG "_B" #BT, rs_matmul_kernel<K, MG, BT>}
 // Specialised variants for the configurations the plugin and BASELINE use,
 // then runtime-k fall-backs (k up to 256).
 const Variant kVariants[] = {
-    RS_VARIANT(10, 4),   // RS(10,4): BASELINE configs 1-4
-    RS_VARIANT(4, 4),    // RS(4,2): plugin default (main.go:34-35)
-    RS_VARIANT(8, 8),    // infectious example RS(8,14)
-    RS_VARIANT(64, 16),  // RS(64,16): BASELINE config 5
-    RS_VARIANT(0, 4),
-    RS_VARIANT(0, 8),
+    RS_VARIANT(10, 4, 256),   // RS(10,4): BASELINE configs 1-4
+    RS_VARIANT(4, 4, 256),    // RS(4,2): plugin default (main.go:34-35)
+    RS_VARIANT(8, 8, 256),    // infectious example RS(8,14)
+    RS_VARIANT(64, 16, 256),  // RS(64,16): BASELINE config 5
+    RS_VARIANT(0, 4, 256),
+    RS_VARIANT(0, 8, 256),
+    // 512/1024-thread blocks measured 3-13% slower for RS(10,4) on one box
+    // (profiles/r01_ab_block.log); RSMI_BLOCK selects among compiled sizes.
 };
 #undef RS_VARIANT
 
 const Variant& pick(int k, int m) {
+    static const int want_bt = [] {
+        const char* e = std::getenv("RSMI_BLOCK");  // tuning knob
+        return e ? std::atoi(e) : 256;
+    }();
+    for (const Variant& v : kVariants)
+        if (v.K != 0 && v.K == k && m <= v.MG && v.BT == want_bt) return v;
     for (const Variant& v : kVariants)
         if (v.K != 0 && v.K == k && m <= v.MG) return v;
     if (k == 64) return kVariants[3];  // RS(64, m > 16): row groups of 16
@@ -342,7 +350,7 @@ const char* variant_name(int k, int m) { return pick(k, m).name; }
 hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     if (a.stripes == 0 || a.ncols16 == 0 || max_e <= 0) return hipSuccess;
     const Variant& v = pick(static_cast<int>(a.k), static_cast<int>(a.m));
-    const uint32_t total_it = (a.ncols16 + kBlock - 1) / kBlock;
+    const uint32_t total_it = (a.ncols16 + v.BT - 1) / v.BT;
     static const uint32_t iters_cap = [] {
         const char* e = std::getenv("RSMI_ITERS");  // tuning knob (default 1: one 4 KiB column chunk per block)
         const int v = e ? std::atoi(e) : 1;
@@ -354,7 +362,7 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     const size_t lds = static_cast<size_t>(a.k) * v.MG * 5 * 4 + a.k * sizeof(void*);
     const uint64_t blocks = a.stripes * a.chunks * a.groups;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-    hipLaunchKernelGGL(v.fn, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), lds, stream, a);
+    hipLaunchKernelGGL(v.fn, dim3(static_cast<uint32_t>(blocks)), dim3(v.BT), lds, stream, a);
     return hipGetLastError();
 }
 

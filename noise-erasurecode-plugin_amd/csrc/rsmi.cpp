@@ -10,12 +10,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <memory>
 #include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "gf256.hpp"
+#include "host_pipeline.hpp"
 #include "rs_kernels.hpp"
 
 namespace {
@@ -115,7 +117,9 @@ struct rs_ctx {
     Staging st_stripe;   // stripe descriptors
     std::vector<uint32_t> scratch_pid, scratch_start;
 
-    // Host-buffer API workspaces.
+    // Host-buffer API: pinned staging pipeline (created on first use) and the
+    // device copy of a decode call's one-pattern table.
+    std::unique_ptr<rsmi::HostPipeline> pipe;
     DevBuf d_work;
     DevBuf d_onepat;
     Staging st_one;
@@ -468,20 +472,18 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    const size_t pitch = round_up(S, 256);
-    if (round_up(S, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;
-    if (!c->d_work.reserve(pitch * static_cast<size_t>(c->n))) return RS_ENOMEM;
-    uint8_t* din = static_cast<uint8_t*>(c->d_work.p);
-    uint8_t* dpar = din + pitch * c->k;
-    hipStream_t s = c->stream;
-    hipError_t e = hipMemcpy2DAsync(din, pitch, input, S, S, c->k, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return RS_EDEVICE;
-    rsmi::MatArgs a = base_args(c, din, 0, dpar, 0, pitch, S, 1);
-    set_patterns(c, 1, c->d_encpat.p, a);
-    e = rsmi::launch_matmul(a, c->m, s);
-    if (e == hipSuccess) e = hipMemcpy2DAsync(parity, S, dpar, pitch, S, c->m, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    return hip_status(e);
+    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
+    if (!c->pipe) return RS_ENOMEM;
+    std::vector<const uint8_t*> srcs(c->k);
+    std::vector<uint8_t*> dsts(c->m);
+    for (int j = 0; j < c->k; ++j) srcs[j] = input + static_cast<size_t>(j) * S;
+    for (int t = 0; t < c->m; ++t) dsts[t] = parity + static_cast<size_t>(t) * S;
+    auto launch = [c](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
+        rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
+        set_patterns(c, 1, c->d_encpat.p, a);
+        return rsmi::launch_matmul(a, c->m, st);
+    };
+    return hip_status(c->pipe->run(srcs.data(), c->k, dsts.data(), c->m, S, launch));
 }
 
 int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t share_len,
@@ -520,49 +522,45 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
         if (present[i] && !by_id[i]) return RS_EINVAL;
     std::vector<int> surv = rsmi::choose_survivors(present.data(), k, n);
     std::vector<int> missing;
-    for (int i = 0; i < k; ++i) {
-        if (present[i])
-            std::memcpy(dst + static_cast<size_t>(i) * share_len, by_id[i], share_len);
-        else
-            missing.push_back(i);
-    }
-    if (missing.empty()) return RS_OK;
+    for (int i = 0; i < k; ++i)
+        if (!present[i]) missing.push_back(i);
     std::vector<uint8_t> rows;
-    if (!rsmi::decode_rows(c->enc, k, n, surv, missing, rows)) return RS_ESINGULAR;
+    if (!missing.empty() && !rsmi::decode_rows(c->enc, k, n, surv, missing, rows)) return RS_ESINGULAR;
 
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
+    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
+    if (!c->pipe) return RS_ENOMEM;
+    hipError_t err = hipSuccess;
     const int e = static_cast<int>(missing.size());
-    const size_t pitch = round_up(share_len, 256);
-    if (round_up(share_len, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;
-    if (!c->d_work.reserve(pitch * static_cast<size_t>(k + e))) return RS_ENOMEM;
-    uint8_t* din = static_cast<uint8_t*>(c->d_work.p);
-    uint8_t* dout = din + pitch * k;
-    // One-pattern table: coef rows, src = slots 0..k-1, dst = k..k+e-1.
-    std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
-    std::copy(rows.begin(), rows.end(), coef.begin());
-    std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(e));
-    for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
-    for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
-    const size_t patbytes = PatLayout(c, 1).total;
-    if (!c->d_onepat.reserve(patbytes) || !c->st_one.acquire(patbytes)) return RS_ENOMEM;
-    uint8_t* hp = static_cast<uint8_t*>(c->st_one.p);
-    pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp);
-    hipStream_t s = c->stream;
-    hipError_t err = hipMemcpyAsync(c->d_onepat.p, hp, patbytes, hipMemcpyHostToDevice, s);
-    for (int i = 0; i < k && err == hipSuccess; ++i)
-        err = hipMemcpyAsync(din + pitch * i, by_id[surv[i]], share_len, hipMemcpyHostToDevice, s);
-    c->st_one.release_after(s);
-    if (err != hipSuccess) return RS_EDEVICE;
-    rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, share_len, 1);
-    set_patterns(c, 1, c->d_onepat.p, a);
-    a.stripe_desc = first_stripe_desc(c, c->d_onepat.p);  // e outputs, not m
-    err = rsmi::launch_matmul(a, e, s);
-    for (int t = 0; t < e && err == hipSuccess; ++t)
-        err = hipMemcpyAsync(dst + static_cast<size_t>(missing[t]) * share_len, dout + pitch * t,
-                             share_len, hipMemcpyDeviceToHost, s);
-    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    if (e > 0) {
+        // One-pattern table: coef rows, src = slots 0..k-1, dst = k..k+e-1.
+        std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
+        std::copy(rows.begin(), rows.end(), coef.begin());
+        std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(e));
+        for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
+        for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
+        std::vector<uint8_t> hp(PatLayout(c, 1).total);
+        pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
+        if (!c->d_onepat.reserve(hp.size())) return RS_ENOMEM;
+        err = hipMemcpy(c->d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice);
+        if (err != hipSuccess) return RS_EDEVICE;
+        std::vector<const uint8_t*> srcs(k);
+        std::vector<uint8_t*> dsts(e);
+        for (int i = 0; i < k; ++i) srcs[i] = by_id[surv[i]];
+        for (int t = 0; t < e; ++t) dsts[t] = dst + static_cast<size_t>(missing[t]) * share_len;
+        auto launch = [c, e](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
+            rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
+            set_patterns(c, 1, c->d_onepat.p, a);
+            a.stripe_desc = first_stripe_desc(c, c->d_onepat.p);  // e outputs, not m
+            return rsmi::launch_matmul(a, e, st);
+        };
+        err = c->pipe->run(srcs.data(), k, dsts.data(), e, share_len, launch);
+    }
+    // present data shares are copied as they are (Rebuild's output callback)
+    for (int i = 0; i < k; ++i)
+        if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * share_len, by_id[i], share_len);
     return hip_status(err);
 }
 
