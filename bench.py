@@ -50,10 +50,10 @@ def parse():
     ap.add_argument("--emin", type=int, default=1)
     ap.add_argument("--emax", type=int, default=None)
     ap.add_argument("--mode", choices=["both", "encode", "reconstruct"], default="both")
-    ap.add_argument("--pattern-pool", type=int, default=-1,
+    ap.add_argument("--pattern-pool", type=int, default=0,
                     help="draw per-stripe erasures from this many distinct patterns "
-                         "(-1: auto = unbounded when all <= emax patterns can be precomputed, "
-                         "else 256)")
+                         "(0: every stripe independent; new patterns are inverted on the "
+                         "GPU inside the timed step)")
     ap.add_argument("--erase", default=None,
                     help="fixed erased shard ids for every stripe, e.g. 0,1,2,3 (default random)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -151,8 +151,6 @@ def main():
     f.fill_splitmix(data.data_ptr(), data.numel(), 0x5EED ^ (rank << 32), sh)
     f.fill_splitmix(parity.data_ptr(), parity.numel(), 1, sh)
     pool = args.pattern_pool
-    if pool < 0:
-        pool = 0 if pattern_total(n, emax) <= (1 << 20) else 256
     if pattern_total(n, emax) <= (1 << 20):
         f.prepare_patterns(emax, sh)  # every pattern inverted + uploaded up front
     rng = np.random.default_rng(0xE4A5 + rank)

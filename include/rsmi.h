@@ -113,6 +113,13 @@ int rs_reconstruct_stripes(rs_ctx *ctx, void *data, size_t data_stripe_stride,
 /* Cached decode patterns held by the ctx (diagnostics / tests). */
 int rs_pattern_count(const rs_ctx *ctx);
 
+/* Diagnostics: the decode rows the engine uses for one erasure pattern
+ * (erased = n flags).  rows receives m*k bytes: row t (t < *count) is the
+ * combination of the k survivors (Rebuild's choice) that regenerates the
+ * t-th erased shard in increasing id order; built on the GPU like every
+ * batched pattern.  Synchronises the ctx's device. */
+int rs_pattern_rows(rs_ctx *ctx, const uint8_t *erased, uint8_t *rows, int *count);
+
 /* Precompute (invert and upload) the decode patterns of every erasure set of
  * 1..max_erasures shards (max_erasures <= m), e.g. the 1,470 patterns of
  * RS(10,4) with <= 4 erasures, so later rs_reconstruct_stripes calls only

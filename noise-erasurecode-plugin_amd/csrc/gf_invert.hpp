@@ -1,0 +1,29 @@
+// gf_invert.hpp -- batched GPU construction of decode rows (gf_invert.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace rsmi {
+
+struct InvertArgs {
+    const uint8_t* enc;      // [n][k] systematic matrix
+    const uint8_t* gf_exp;   // [512] 2^i (i < 510)
+    const uint8_t* gf_log;   // [256]
+    const uint32_t* src;     // [npat][k] survivor ids
+    const uint32_t* dst;     // [npat][dst_stride] erased ids
+    const uint32_t* cnt;     // [npat] erased count
+    uint32_t dst_stride;
+    uint8_t* coef;           // [npat][m][k] decode rows (output)
+    uint32_t first;          // first pattern id to build
+    uint32_t k, m;
+    uint32_t* status;        // bit 0 set if a survivor matrix was singular
+};
+
+// Builds patterns [first, first + count): one workgroup each.
+hipError_t launch_invert(const InvertArgs& a, uint32_t count, hipStream_t stream);
+size_t invert_lds_bytes(int k, int m);
+
+}  // namespace rsmi

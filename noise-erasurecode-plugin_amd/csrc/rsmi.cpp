@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "gf256.hpp"
+#include "gf_invert.hpp"
 #include "host_pipeline.hpp"
 #include "rs_kernels.hpp"
 
@@ -52,6 +53,31 @@ struct DevBuf {
         }
         size_t want = std::max({bytes, size_t(4096), 2 * cap});
         if (hipMalloc(&p, want) != hipSuccess) return false;
+        cap = want;
+        return true;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// A growable device buffer whose first `used` bytes survive growth.
+struct GrowBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool reserve_keep(size_t bytes, size_t used, hipStream_t s) {
+        if (bytes <= cap) return true;
+        const size_t want = std::max({bytes, size_t(4096), 2 * cap});
+        void* np = nullptr;
+        if (hipMalloc(&np, want) != hipSuccess) return false;
+        if (p) {
+            if (used) (void)hipMemcpyAsync(np, p, std::min(used, cap), hipMemcpyDeviceToDevice, s);
+            (void)hipDeviceSynchronize();  // older launches may still read p
+            (void)hipFree(p);
+        }
+        p = np;
         cap = want;
         return true;
     }
@@ -106,12 +132,14 @@ struct rs_ctx {
     // Encode pattern on the device (PatBlob layout, one pattern).
     DevBuf d_encpat;
 
-    // Decode-pattern cache (host mirror + device copy of every pattern).
+    // Decode-pattern cache.  The host keeps each pattern's survivor / erased
+    // ids; the device holds the same plus its decode rows, which the GPU
+    // builds (gf_invert.hip) when a pattern is first seen.
     std::unordered_map<std::string, int> pat_index;
-    std::vector<uint8_t> h_coef;
-    std::vector<uint32_t> h_src, h_dst, h_cnt;
-    DevBuf d_pats;
-    size_t uploaded = 0;  // patterns present on the device
+    std::vector<uint32_t> h_src, h_dst, h_cnt;  // [npat][k], [npat][dst_stride], [npat]
+    GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt;
+    size_t uploaded = 0;  // patterns built on the device
+    DevBuf d_gf;          // enc [n][k] | gf exp [512] | gf log [256] | status u32
     DevBuf d_stripe_pat;
     Staging st_pat;      // pattern-table uploads
     Staging st_stripe;   // stripe descriptors
@@ -222,18 +250,11 @@ int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
         return -1;
     }
     std::vector<int> surv = rsmi::choose_survivors(present.data(), c->k, c->n);
-    std::vector<uint8_t> rows;
-    if (!targets.empty() && !rsmi::decode_rows(c->enc, c->k, c->n, surv, targets, rows)) {
-        *err = RS_ESINGULAR;
-        return -1;
-    }
     const int id = static_cast<int>(c->pat_index.size());
-    const size_t mk = static_cast<size_t>(c->m) * c->k;
-    c->h_coef.resize((id + 1) * mk, 0);
-    std::copy(rows.begin(), rows.end(), c->h_coef.begin() + id * mk);
     for (int v : surv) c->h_src.push_back(static_cast<uint32_t>(v));
-    for (int t = 0; t < c->m; ++t)
-        c->h_dst.push_back(t < static_cast<int>(targets.size()) ? static_cast<uint32_t>(targets[t]) : 0u);
+    const size_t ds = dst_stride(c);
+    for (size_t t = 0; t < ds; ++t)
+        c->h_dst.push_back(t < targets.size() ? static_cast<uint32_t>(targets[t]) : 0u);
     c->h_cnt.push_back(static_cast<uint32_t>(targets.size()));
     c->pat_index.emplace(std::move(key), id);
     return id;
@@ -243,26 +264,70 @@ int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
 void reset_patterns(rs_ctx* c) {
     (void)hipDeviceSynchronize();
     c->pat_index.clear();
-    c->h_coef.clear();
     c->h_src.clear();
     c->h_dst.clear();
     c->h_cnt.clear();
     c->uploaded = 0;
 }
 
-int upload_patterns(rs_ctx* c, hipStream_t s) {
-    const size_t npat = c->h_cnt.size();
-    if (npat == c->uploaded) return RS_OK;
-    PatLayout L(c, npat);
-    if (!c->d_pats.reserve(L.total)) return RS_ENOMEM;
-    if (!c->st_pat.acquire(L.total)) return RS_ENOMEM;
+const uint8_t* dev_enc(rs_ctx* c) { return static_cast<const uint8_t*>(c->d_gf.p); }
+uint32_t* dev_status(rs_ctx* c) {
+    return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_gf.p) +
+                                       round_up(static_cast<size_t>(c->n) * c->k + 768, 16));
+}
+
+// Uploads the ids of patterns created since the last flush and builds their
+// decode rows on the GPU (one workgroup per pattern), in stream order.
+int flush_patterns(rs_ctx* c, hipStream_t s) {
+    const size_t npat = c->h_cnt.size(), first = c->uploaded;
+    if (npat == first) return RS_OK;
+    const size_t k = c->k, m = c->m, ds = dst_stride(c);
+    if (!c->d_pcoef.reserve_keep(npat * m * k, first * m * k, s) ||
+        !c->d_psrc.reserve_keep(npat * k * 4, first * k * 4, s) ||
+        !c->d_pdst.reserve_keep(npat * ds * 4, first * ds * 4, s) ||
+        !c->d_pcnt.reserve_keep(npat * 4, first * 4, s))
+        return RS_ENOMEM;
+    const size_t cnt = npat - first;
+    const size_t b_src = cnt * k * 4, b_dst = cnt * ds * 4, b_cnt = cnt * 4;
+    if (!c->st_pat.acquire(b_src + b_dst + b_cnt)) return RS_ENOMEM;
     uint8_t* h = static_cast<uint8_t*>(c->st_pat.p);
-    pack_patterns(c, npat, c->h_coef.data(), c->h_src.data(), c->h_dst.data(), c->h_cnt.data(), h);
-    hipError_t e = hipMemcpyAsync(c->d_pats.p, h, L.total, hipMemcpyHostToDevice, s);
+    std::memcpy(h, c->h_src.data() + first * k, b_src);
+    std::memcpy(h + b_src, c->h_dst.data() + first * ds, b_dst);
+    std::memcpy(h + b_src + b_dst, c->h_cnt.data() + first, b_cnt);
+    hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(c->d_psrc.p) + first * k * 4, h, b_src,
+                                  hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(static_cast<uint8_t*>(c->d_pdst.p) + first * ds * 4, h + b_src, b_dst,
+                           hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(static_cast<uint8_t*>(c->d_pcnt.p) + first * 4, h + b_src + b_dst, b_cnt,
+                           hipMemcpyHostToDevice, s);
     c->st_pat.release_after(s);
+    if (e != hipSuccess) return RS_EDEVICE;
+    rsmi::InvertArgs ia{};
+    ia.enc = dev_enc(c);
+    ia.gf_exp = dev_enc(c) + static_cast<size_t>(c->n) * c->k;
+    ia.gf_log = ia.gf_exp + 512;
+    ia.src = static_cast<const uint32_t*>(c->d_psrc.p);
+    ia.dst = static_cast<const uint32_t*>(c->d_pdst.p);
+    ia.cnt = static_cast<const uint32_t*>(c->d_pcnt.p);
+    ia.dst_stride = static_cast<uint32_t>(ds);
+    ia.coef = static_cast<uint8_t*>(c->d_pcoef.p);
+    ia.first = static_cast<uint32_t>(first);
+    ia.k = static_cast<uint32_t>(c->k);
+    ia.m = static_cast<uint32_t>(c->m);
+    ia.status = dev_status(c);
+    e = rsmi::launch_invert(ia, static_cast<uint32_t>(cnt), s);
     if (e != hipSuccess) return RS_EDEVICE;
     c->uploaded = npat;
     return RS_OK;
+}
+
+void set_cache_patterns(rs_ctx* c, rsmi::MatArgs& a) {
+    a.coef = static_cast<const uint8_t*>(c->d_pcoef.p);
+    a.src = static_cast<const uint32_t*>(c->d_psrc.p);
+    a.dst = static_cast<const uint32_t*>(c->d_pdst.p);
+    a.dst_stride = static_cast<uint32_t>(dst_stride(c));
 }
 
 }  // namespace
@@ -316,6 +381,20 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     std::vector<uint8_t> pat(PatLayout(c, 1).total);
     pack_patterns(c, 1, c->enc.data() + static_cast<size_t>(k) * k, src.data(), dst.data(),
                   cnt.data(), pat.data());
+    {
+        const rsmi::Field& F = rsmi::field();
+        const size_t nk = static_cast<size_t>(n) * k;
+        std::vector<uint8_t> gf(round_up(nk + 768, 16) + 16, 0);
+        std::copy(c->enc.begin(), c->enc.end(), gf.begin());
+        std::memcpy(gf.data() + nk, F.exp, 510);
+        std::memcpy(gf.data() + nk + 510, F.exp, 2);
+        std::memcpy(gf.data() + nk + 512, F.log, 256);
+        if (!c->d_gf.reserve(gf.size()) ||
+            hipMemcpy(c->d_gf.p, gf.data(), gf.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            rs_free(c);
+            return RS_EDEVICE;
+        }
+    }
     if (!c->d_encpat.reserve(pat.size()) ||
         hipMemcpy(c->d_encpat.p, pat.data(), pat.size(), hipMemcpyHostToDevice) != hipSuccess) {
         rs_free(c);
@@ -340,8 +419,9 @@ void rs_free(rs_ctx* c) {
         c->st_pat.destroy();
         c->st_stripe.destroy();
         c->st_one.destroy();
-        for (DevBuf* b : {&c->d_encpat, &c->d_pats, &c->d_stripe_pat, &c->d_work, &c->d_onepat})
+        for (DevBuf* b : {&c->d_encpat, &c->d_stripe_pat, &c->d_work, &c->d_onepat, &c->d_gf})
             b->release();
+        for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt}) b->release();
         if (c->stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -359,6 +439,26 @@ int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
 
 int rs_pattern_count(const rs_ctx* c) {
     return c ? static_cast<int>(c->pat_index.size()) : RS_EINVAL;
+}
+
+int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count) {
+    if (!c || !erased || !rows || !count) return RS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    int err = RS_OK;
+    const int id = pattern_for(c, erased, &err);
+    if (id < 0) return err;
+    int st = flush_patterns(c, c->stream);
+    if (st != RS_OK) return st;
+    const size_t mk = static_cast<size_t>(c->m) * c->k;
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(rows, static_cast<uint8_t*>(c->d_pcoef.p) + id * mk, mk, hipMemcpyDeviceToHost) != hipSuccess)
+        return RS_EDEVICE;
+    *count = static_cast<int>(c->h_cnt[id]);
+    uint32_t status = 0;
+    if (hipMemcpy(&status, dev_status(c), 4, hipMemcpyDeviceToHost) != hipSuccess) return RS_EDEVICE;
+    return status ? RS_ESINGULAR : RS_OK;
 }
 
 int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
@@ -390,9 +490,12 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
             for (int j = i + 1; j < e; ++j) idx[j] = idx[j - 1] + 1;
         }
     }
-    int st = upload_patterns(c, static_cast<hipStream_t>(stream));
+    int st = flush_patterns(c, static_cast<hipStream_t>(stream));
     if (st != RS_OK) return st;
-    return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return RS_EDEVICE;
+    uint32_t status = 0;
+    if (hipMemcpy(&status, dev_status(c), 4, hipMemcpyDeviceToHost) != hipSuccess) return RS_EDEVICE;
+    return status ? RS_ESINGULAR : RS_OK;
 }
 
 int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, size_t pss,
@@ -450,7 +553,7 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
         const uint32_t p = pid[i];
         if (c->h_cnt[p]) desc[start[bucket(i)]++] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
     }
-    int st = upload_patterns(c, s);
+    int st = flush_patterns(c, s);
     if (st != RS_OK) return st;
     if (!c->d_stripe_pat.reserve(used * sizeof(uint2))) return RS_ENOMEM;
     hipError_t e = hipMemcpyAsync(c->d_stripe_pat.p, desc, used * sizeof(uint2),
@@ -458,7 +561,7 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     c->st_stripe.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
     rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used);
-    set_patterns(c, c->h_cnt.size(), c->d_pats.p, a);
+    set_cache_patterns(c, a);
     a.stripe_desc = static_cast<const uint2*>(c->d_stripe_pat.p);
     return hip_status(rsmi::launch_matmul(a, max_e, s));
 }

@@ -35,6 +35,7 @@ EXPORTS = (
     "rs_new", "rs_new_on_device", "rs_free", "rs_k", "rs_n", "rs_device",
     "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode",
     "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_prepare_patterns",
+    "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
     "rs_stream_sync", "rs_fill_splitmix",
 )
@@ -81,6 +82,7 @@ def _lib() -> ctypes.CDLL:
             "rs_reconstruct_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp, vp]),
             "rs_pattern_count": (i32, [vp]),
             "rs_prepare_patterns": (i32, [vp, i32, vp]),
+            "rs_pattern_rows": (i32, [vp, vp, vp, ctypes.POINTER(i32)]),
             "rs_pinned_alloc": (vp, [sz]),
             "rs_pinned_free": (None, [vp]),
             "rs_device_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
@@ -238,6 +240,17 @@ class FEC:
 
     def pattern_count(self) -> int:
         return _lib().rs_pattern_count(self._h)
+
+    def pattern_rows(self, erased: bytes):
+        """(rows bytes m*k, count) the engine uses for this erasure pattern."""
+        m = self.n - self.k
+        buf = (ctypes.c_uint8 * max(m * self.k, 1))()
+        cnt = ctypes.c_int()
+        flags = ctypes.c_char_p(bytes(erased))
+        _check(_lib().rs_pattern_rows(self._h, ctypes.cast(flags, ctypes.c_void_p),
+                                      ctypes.cast(buf, ctypes.c_void_p), ctypes.byref(cnt)),
+               "rs_pattern_rows")
+        return bytes(buf)[:m * self.k], cnt.value
 
     def prepare_patterns(self, max_erasures: int, stream: int = 0) -> None:
         _check(_lib().rs_prepare_patterns(self._h, max_erasures, stream or None),
