@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--emin", type=int, default=1)
     ap.add_argument("--emax", type=int, default=None)
     ap.add_argument("--mode", choices=["both", "encode", "reconstruct"], default="both")
+    ap.add_argument("--placement", choices=["local", "sharded"], default="local",
+                    help="local: stripe s on rank s mod N (headline). sharded: shard i of "
+                         "every stripe on rank i mod N; a step gathers each stripe's k "
+                         "survivors to its owner over RCCL, then reconstructs (configs[3])")
     ap.add_argument("--pattern-pool", type=int, default=0,
                     help="draw per-stripe erasures from this many distinct patterns "
                          "(0: every stripe independent; new patterns are inverted on the "
@@ -128,13 +132,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    torch.cuda.set_device(local)
+    distributed = "RANK" in os.environ  # launched by torch.distributed.run (any N)
+    if distributed:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.placement == "sharded":
+        return sharded_main(args, world, rank, local, dev, distributed)
 
     import rsmi
 
@@ -188,18 +193,18 @@ def main():
     for i in range(args.warmup):
         step(i, False)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i, True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         torch.distributed.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -276,7 +281,90 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
+        torch.distributed.destroy_process_group()
+
+
+def sharded_main(args, world, rank, local, dev, distributed):
+    """configs[3], shard-distributed placement: shard i of every stripe is
+    held by rank i mod N (the p2p analogue of main.go:207 broadcasting each
+    shard to peers).  One step = the RCCL survivor gather (one grouped
+    send/recv, rsmi/distributed.py) + rs_reconstruct_stripes of the stripes
+    this rank owns.  Reported against the xGMI roofline (gathered bytes)."""
+    import rsmi
+    from rsmi import distributed as rd
+
+    k, n, S = args.k, args.n, args.shard
+    m = n - k
+    emax = args.emax if args.emax is not None else m
+    gstripes = args.stripes * world          # global stripes; each rank owns args.stripes
+    f = rsmi.FEC(k, n, device=local)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    ids = rd.local_shard_ids(rank, n, world)
+    held = torch.empty((gstripes, len(ids), S), dtype=torch.uint8, device=dev)
+    # Setup (untimed): every rank encodes the global stripes in batches and
+    # keeps its shard ids (deterministic seeds, so all ranks agree).
+    batch = 64
+    tmp_d = torch.empty(batch * k * S, dtype=torch.uint8, device=dev)
+    tmp_p = torch.empty(batch * m * S, dtype=torch.uint8, device=dev)
+    for b0 in range(0, gstripes, batch):
+        nb = min(batch, gstripes - b0)
+        f.fill_splitmix(tmp_d.data_ptr(), nb * k * S, 0x5EED + b0, sh)
+        f.encode_stripes(tmp_d.data_ptr(), k * S, tmp_p.data_ptr(), m * S, S, S, nb, sh)
+        full = torch.cat([tmp_d[:nb * k * S].view(nb, k, S), tmp_p[:nb * m * S].view(nb, m, S)], 1)
+        held[b0:b0 + nb] = full[:, ids, :]
+    if pattern_total(n, emax) <= (1 << 20):
+        f.prepare_patterns(emax, sh)
+    torch.cuda.synchronize(dev)
+    rng = np.random.default_rng(0xE4A5)  # same erasure map on every rank
+    ersets = erasure_sets(rng, args.warmup + args.steps, gstripes, n, args.emin, emax,
+                          args.pattern_pool)
+    plans = [rd.plan_exchange(er, k, n, rank, world, S) for er in ersets]
+
+    def step(i):
+        out = rd.gather_survivors(held, plans[i], n)
+        owned = plans[i].owned
+        rd.reconstruct_owned(f, out, ersets[i][owned], sh)
+        return out
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    rec_bytes = sum(int(((k + ersets[i][plans[i].owned].sum(axis=1)) * S).sum())
+                    for i in range(args.warmup, args.warmup + args.steps))
+    xgmi_bytes = sum(plans[i].bytes_in for i in range(args.warmup, args.warmup + args.steps))
+    vals = torch.tensor([elapsed, rec_bytes, xgmi_bytes], dtype=torch.float64, device=dev)
+    if distributed:
+        mx = vals[:1].clone()
+        torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(vals, op=torch.distributed.ReduceOp.SUM)
+        vals[0] = mx[0]
+    elapsed, rec_total, xgmi_total = (float(v) for v in vals.tolist())
+    if rank == 0:
+        xg = xgmi_total / elapsed / 1e9
+        print(json.dumps({
+            "metric": "RS(10,4) reconstruct GB/s with RCCL survivor gather (configs[3], sharded)",
+            "value": round(rec_total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"RS({k},{n}) {args.emin}-{emax}-erasure reconstruct, shard i "
+                                   f"on rank i mod N, {args.stripes} owned stripes x {S} B shards "
+                                   "per rank", "placement": "sharded"},
+            "xgmi": {"gathered_GB": round(xgmi_total / 1e9, 3), "achieved_GBps_total": round(xg, 1),
+                     "per_rank_GBps": round(xg / max(world, 1), 1),
+                     "link_peak_GBps": 153.0, "links_per_gpu": 7},
+        }), flush=True)
+    if distributed:
         torch.distributed.destroy_process_group()
 
 
