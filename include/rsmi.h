@@ -45,6 +45,7 @@ typedef enum {
     RS_EINVAL = -8,            /* bad argument (NULL, misaligned device buffer...) */
     RS_EDEVICE = -9,           /* HIP runtime error or no gfx950 device            */
     RS_ENOMEM = -10,           /* host or device allocation failed                 */
+    RS_ETOO_MANY_ERRORS = -16, /* Correct: TooManyErrors (Berlekamp-Welch failed)  */
 } rs_status;
 
 typedef struct rs_ctx rs_ctx;
@@ -72,14 +73,20 @@ const char *rs_strerror(int status);
  * parity[(i-k)*S, (i-k+1)*S).  len == 0 is allowed (empty shares). */
 int rs_encode(rs_ctx *ctx, const uint8_t *input, size_t len, uint8_t *parity);
 
-/* rs_decode replaces (*FEC).Decode(dst, shares) at main.go:77 (the Correct
- * step is a no-op for exactly k distinct shares, the only case the plugin
- * produces: main.go:65).  numbers[count] / shares[count] describe the
- * received infectious.Share values; both arrays are sorted in place by
- * number, like infectious sorts the caller's slice.  Each share holds
- * share_len bytes.  dst receives k * share_len bytes = the original input.
+/* rs_decode replaces (*FEC).Decode(dst, shares) at main.go:77: Correct, then
+ * Rebuild.  numbers[count] / shares[count] describe the received
+ * infectious.Share values; both arrays are sorted in place by number, like
+ * infectious sorts the caller's slice.  Each share holds share_len bytes.
+ * dst receives k * share_len bytes = the original input.
+ * With exactly k distinct shares (the only case the plugin produces,
+ * main.go:65) Correct has nothing to check.  With more, shares inconsistent
+ * with one codeword are corrected by Berlekamp-Welch (up to
+ * floor((count-k)/2) bad shares per byte column); the corrections go to dst
+ * only -- unlike infectious, the caller's share bytes are not modified.
  * Errors: count < k -> RS_ENOT_ENOUGH; number outside [0, n) ->
- * RS_EBAD_SHARE_ID; fewer than k distinct numbers -> RS_ESINGULAR. */
+ * RS_EBAD_SHARE_ID; fewer than k distinct numbers -> RS_ESINGULAR;
+ * inconsistent shares with count - k < 2 -> RS_ENOT_ENOUGH; no codeword
+ * within the correction radius -> RS_ETOO_MANY_ERRORS. */
 int rs_decode(rs_ctx *ctx, int *numbers, const uint8_t **shares, int count,
               size_t share_len, uint8_t *dst);
 

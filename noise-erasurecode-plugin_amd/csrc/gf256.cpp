@@ -128,6 +128,80 @@ bool decode_rows(const std::vector<uint8_t>& enc, int k, int n, const std::vecto
     return true;
 }
 
+int bw_column(int k, int n, const int* nums, const uint8_t* ys, int r, uint8_t* out) {
+    const Field& f = field();
+    for (int t = 1; 2 * t <= r - k; ++t) {
+        // Unknowns: Q's k+t coefficients, E's t low coefficients (E monic).
+        // Row i: sum_j q_j x^j + y sum_l e_l x^l = y x^t   (char 2)
+        const int nq = k + t, cols = nq + t, w = cols + 1;
+        std::vector<uint8_t> A(static_cast<size_t>(r) * w);
+        for (int i = 0; i < r; ++i) {
+            const uint8_t x = eval_point(nums[i]), y = ys[i];
+            uint8_t* row = &A[static_cast<size_t>(i) * w];
+            uint8_t xp = 1;
+            for (int j = 0; j < nq; ++j) {
+                row[j] = xp;
+                if (j < t) row[nq + j] = f.mul[y][xp];
+                if (j == t) row[cols] = f.mul[y][xp];
+                xp = f.mul[xp][x];
+            }
+            if (t >= nq) row[cols] = f.mul[y][gpow(x, t)];
+        }
+        // reduced row echelon form
+        std::vector<int> pivcol;
+        int rank = 0;
+        for (int col = 0; col < cols && rank < r; ++col) {
+            int p = -1;
+            for (int i = rank; i < r; ++i)
+                if (A[static_cast<size_t>(i) * w + col]) { p = i; break; }
+            if (p < 0) continue;
+            if (p != rank)
+                for (int j = 0; j < w; ++j) std::swap(A[static_cast<size_t>(p) * w + j], A[static_cast<size_t>(rank) * w + j]);
+            uint8_t* pr = &A[static_cast<size_t>(rank) * w];
+            const uint8_t inv = f.inv[pr[col]];
+            for (int j = 0; j < w; ++j) pr[j] = f.mul[inv][pr[j]];
+            for (int i = 0; i < r; ++i) {
+                uint8_t* ri = &A[static_cast<size_t>(i) * w];
+                if (i == rank || !ri[col]) continue;
+                const uint8_t fac = ri[col];
+                for (int j = 0; j < w; ++j) ri[j] ^= f.mul[fac][pr[j]];
+            }
+            pivcol.push_back(col);
+            ++rank;
+        }
+        bool consistent = true;
+        for (int i = rank; i < r && consistent; ++i)
+            if (A[static_cast<size_t>(i) * w + cols]) consistent = false;
+        if (!consistent) continue;
+        std::vector<uint8_t> u(cols, 0);  // one solution, free variables 0
+        for (int i = 0; i < rank; ++i) u[pivcol[i]] = A[static_cast<size_t>(i) * w + cols];
+        // P = Q / E by long division (E monic, degree t)
+        std::vector<uint8_t> q(u.begin(), u.begin() + nq), e(t + 1), p(k, 0);
+        for (int l = 0; l < t; ++l) e[l] = u[nq + l];
+        e[t] = 1;
+        for (int d = nq - 1; d >= t; --d) {
+            const uint8_t cf = q[d];
+            p[d - t] = cf;
+            if (cf)
+                for (int l = 0; l <= t; ++l) q[d - t + l] ^= f.mul[cf][e[l]];
+        }
+        bool rem = false;
+        for (int d = 0; d < t; ++d) rem |= q[d] != 0;
+        if (rem) continue;
+        auto eval = [&](uint8_t x) {
+            uint8_t v = 0;
+            for (int d = k - 1; d >= 0; --d) v = f.mul[v][x] ^ p[d];
+            return v;
+        };
+        int bad = 0;
+        for (int i = 0; i < r; ++i) bad += eval(eval_point(nums[i])) != ys[i];
+        if (bad > t) continue;
+        for (int i = 0; i < n; ++i) out[i] = eval(eval_point(i));
+        return bad;
+    }
+    return -1;
+}
+
 void coef_tables(uint8_t c, uint32_t w[5]) {
     const Field& f = field();
     auto pack = [&](int base, int step, int count) {

@@ -50,6 +50,14 @@ bool decode_rows(const std::vector<uint8_t>& enc, int k, int n,
                  const std::vector<int>& survivors, const std::vector<int>& targets,
                  std::vector<uint8_t>& rows_out);
 
+// Berlekamp-Welch on one byte column (infectious Correct): nums[r] share
+// numbers with received bytes ys[r].  Finds the nearest codeword within
+// floor((r-k)/2) errors and writes its symbol for every share number to
+// out[n]; returns the number of received symbols it disagrees with, or -1 if
+// there is no such codeword.  Codeword symbol i is P(x_i) for a polynomial P
+// of degree < k, x_0 = 0, x_i = 2^i (the systematic code's evaluation view).
+int bw_column(int k, int n, const int* nums, const uint8_t* ys, int r, uint8_t* out);
+
 // Split-table words for one coefficient c, as the HIP kernels consume them
 // with v_perm_b32: w[0..1] = c*{0..7}, w[2..3] = c*{0,8,..,56},
 // w[4] = c*{0,64,128,192} (byte i of each word = entry i).

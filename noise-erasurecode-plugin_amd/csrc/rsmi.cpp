@@ -330,6 +330,163 @@ void set_cache_patterns(rs_ctx* c, rsmi::MatArgs& a) {
     a.dst_stride = static_cast<uint32_t>(dst_stride(c));
 }
 
+// out_t = decode row (surv -> targets[t]) applied to the survivors, on the
+// GPU through the pinned host pipeline.  Caller holds c->mu on c->device.
+int gpu_rows(rs_ctx* c, const std::vector<int>& surv, const std::vector<const uint8_t*>& surv_ptr,
+             const std::vector<int>& targets, const std::vector<uint8_t*>& outs, size_t S) {
+    const int k = c->k, e = static_cast<int>(targets.size());
+    if (e == 0 || S == 0) return RS_OK;
+    std::vector<uint8_t> rows;
+    if (!rsmi::decode_rows(c->enc, k, c->n, surv, targets, rows)) return RS_ESINGULAR;
+    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
+    if (!c->pipe) return RS_ENOMEM;
+    // A launch codes at most m rows per group of the one-pattern table; more
+    // targets (possible when correcting) go in several passes.
+    for (int t0 = 0; t0 < e; t0 += c->m) {
+        const int et = std::min(c->m, e - t0);
+        std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
+        std::copy(rows.begin() + static_cast<size_t>(t0) * k,
+                  rows.begin() + static_cast<size_t>(t0 + et) * k, coef.begin());
+        std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(et));
+        for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
+        for (int t = 0; t < et; ++t) dstid[t] = static_cast<uint32_t>(k + t);
+        std::vector<uint8_t> hp(PatLayout(c, 1).total);
+        pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
+        if (!c->d_onepat.reserve(hp.size())) return RS_ENOMEM;
+        if (hipMemcpy(c->d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return RS_EDEVICE;
+        auto launch = [c, et](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
+            rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
+            set_patterns(c, 1, c->d_onepat.p, a);
+            a.stripe_desc = first_stripe_desc(c, c->d_onepat.p);  // et outputs, not m
+            return rsmi::launch_matmul(a, et, st);
+        };
+        const hipError_t err =
+            c->pipe->run(surv_ptr.data(), k, outs.data() + t0, et, S, launch);
+        if (err != hipSuccess) return RS_EDEVICE;
+    }
+    return RS_OK;
+}
+
+// Rebuild from the present shares: data shares copied, missing ones
+// regenerated from Rebuild's survivors.
+int rebuild_into(rs_ctx* c, const std::vector<uint8_t>& present,
+                 const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst) {
+    const int k = c->k;
+    std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
+    std::vector<const uint8_t*> sp(k);
+    for (int i = 0; i < k; ++i) sp[i] = by_id[surv[i]];
+    std::vector<int> missing;
+    std::vector<uint8_t*> outs;
+    for (int i = 0; i < k; ++i)
+        if (!present[i]) {
+            missing.push_back(i);
+            outs.push_back(dst + static_cast<size_t>(i) * S);
+        }
+    const int st = gpu_rows(c, surv, sp, missing, outs, S);
+    if (st != RS_OK) return st;
+    for (int i = 0; i < k; ++i)
+        if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
+    return RS_OK;
+}
+
+// Columns where any of `outs` differs from the received shares `recv`.
+std::vector<size_t> mismatched_columns(const std::vector<std::vector<uint8_t>>& outs,
+                                       const std::vector<const uint8_t*>& recv, size_t S) {
+    std::vector<uint8_t> bad(S, 0);
+    for (size_t t = 0; t < outs.size(); ++t) {
+        const uint8_t* a = outs[t].data();
+        const uint8_t* b = recv[t];
+        for (size_t o = 0; o < S; o += 4096) {
+            const size_t w = std::min<size_t>(4096, S - o);
+            if (std::memcmp(a + o, b + o, w) == 0) continue;
+            for (size_t j = o; j < o + w; ++j) bad[j] |= a[j] != b[j];
+        }
+    }
+    std::vector<size_t> cols;
+    for (size_t j = 0; j < S; ++j)
+        if (bad[j]) cols.push_back(j);
+    return cols;
+}
+
+// infectious Decode with more than k distinct shares: Correct (consistency
+// check + Berlekamp-Welch on inconsistent columns) then Rebuild.  The bulk
+// work is GPU decodes; Berlekamp-Welch runs on the host for one column to
+// locate the bad shares, which are then treated as erasures, and again only
+// for columns that stay inconsistent.  Unlike infectious, the caller's share
+// bytes are not modified (the corrected values only land in dst).
+int correct_decode(rs_ctx* c, std::vector<uint8_t> present, const std::vector<const uint8_t*>& by_id,
+                   size_t S, uint8_t* dst) {
+    const int k = c->k, n = c->n;
+    std::vector<int> P;
+    for (int i = 0; i < n; ++i)
+        if (present[i]) P.push_back(i);
+    const int r = static_cast<int>(P.size());
+    // 1. are the shares one codeword?  predict the extras from Rebuild's k
+    std::vector<int> base = rsmi::choose_survivors(present.data(), k, n);
+    std::vector<uint8_t> in_base(n, 0);
+    for (int v : base) in_base[v] = 1;
+    std::vector<int> extras;
+    for (int i : P)
+        if (!in_base[i]) extras.push_back(i);
+    std::vector<const uint8_t*> bp(k);
+    for (int i = 0; i < k; ++i) bp[i] = by_id[base[i]];
+    std::vector<std::vector<uint8_t>> pred(extras.size(), std::vector<uint8_t>(S));
+    std::vector<uint8_t*> po;
+    std::vector<const uint8_t*> rx;
+    for (size_t t = 0; t < extras.size(); ++t) {
+        po.push_back(pred[t].data());
+        rx.push_back(by_id[extras[t]]);
+    }
+    int st = gpu_rows(c, base, bp, extras, po, S);
+    if (st != RS_OK) return st;
+    std::vector<size_t> bad = mismatched_columns(pred, rx, S);
+    if (bad.empty()) return rebuild_into(c, present, by_id, S, dst);
+    if ((r - k) / 2 <= 0) return RS_ENOT_ENOUGH;  // berlekampWelch: e <= 0
+    // 2. locate the bad shares on the first inconsistent column
+    std::vector<uint8_t> ys(r), cw(n);
+    auto column = [&](size_t j) {
+        for (int i = 0; i < r; ++i) ys[i] = by_id[P[i]][j];
+        return rsmi::bw_column(k, n, P.data(), ys.data(), r, cw.data());
+    };
+    if (column(bad[0]) < 0) return RS_ETOO_MANY_ERRORS;
+    std::vector<uint8_t> present2 = present;
+    for (int i = 0; i < r; ++i)
+        if (cw[P[i]] != ys[i]) present2[P[i]] = 0;  // treat as erased
+    // 3. rebuild from the rest; shares outside its survivors must agree
+    std::vector<int> base2 = rsmi::choose_survivors(present2.data(), k, n);
+    std::vector<uint8_t> in_b2(n, 0);
+    for (int v : base2) in_b2[v] = 1;
+    std::vector<int> targets, others;
+    std::vector<uint8_t*> outs;
+    for (int i = 0; i < k; ++i)
+        if (!in_b2[i]) {
+            targets.push_back(i);
+            outs.push_back(dst + static_cast<size_t>(i) * S);
+        }
+    for (int i : P)
+        if (present2[i] && !in_b2[i]) others.push_back(i);
+    std::vector<std::vector<uint8_t>> chk(others.size(), std::vector<uint8_t>(S));
+    std::vector<const uint8_t*> rx2;
+    for (size_t t = 0; t < others.size(); ++t) {
+        targets.push_back(others[t]);
+        outs.push_back(chk[t].data());
+        rx2.push_back(by_id[others[t]]);
+    }
+    std::vector<const uint8_t*> bp2(k);
+    for (int i = 0; i < k; ++i) bp2[i] = by_id[base2[i]];
+    st = gpu_rows(c, base2, bp2, targets, outs, S);
+    if (st != RS_OK) return st;
+    for (int i = 0; i < k; ++i)
+        if (in_b2[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
+    // 4. columns still inconsistent: full Berlekamp-Welch each
+    for (size_t j : mismatched_columns(chk, rx2, S)) {
+        if (column(j) < 0) return RS_ETOO_MANY_ERRORS;
+        for (int i = 0; i < k; ++i) dst[static_cast<size_t>(i) * S + j] = cw[i];
+    }
+    return RS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -347,6 +504,7 @@ const char* rs_strerror(int st) {
         case RS_EINVAL: return "invalid argument";
         case RS_EDEVICE: return "HIP device error";
         case RS_ENOMEM: return "out of memory";
+        case RS_ETOO_MANY_ERRORS: return "too many errors to reconstruct";
         default: return "unknown error";
     }
 }
@@ -623,48 +781,11 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (share_len == 0) return RS_OK;
     for (int i = 0; i < n; ++i)
         if (present[i] && !by_id[i]) return RS_EINVAL;
-    std::vector<int> surv = rsmi::choose_survivors(present.data(), k, n);
-    std::vector<int> missing;
-    for (int i = 0; i < k; ++i)
-        if (!present[i]) missing.push_back(i);
-    std::vector<uint8_t> rows;
-    if (!missing.empty() && !rsmi::decode_rows(c->enc, k, n, surv, missing, rows)) return RS_ESINGULAR;
-
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
-    if (!c->pipe) return RS_ENOMEM;
-    hipError_t err = hipSuccess;
-    const int e = static_cast<int>(missing.size());
-    if (e > 0) {
-        // One-pattern table: coef rows, src = slots 0..k-1, dst = k..k+e-1.
-        std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
-        std::copy(rows.begin(), rows.end(), coef.begin());
-        std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(e));
-        for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
-        for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
-        std::vector<uint8_t> hp(PatLayout(c, 1).total);
-        pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
-        if (!c->d_onepat.reserve(hp.size())) return RS_ENOMEM;
-        err = hipMemcpy(c->d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice);
-        if (err != hipSuccess) return RS_EDEVICE;
-        std::vector<const uint8_t*> srcs(k);
-        std::vector<uint8_t*> dsts(e);
-        for (int i = 0; i < k; ++i) srcs[i] = by_id[surv[i]];
-        for (int t = 0; t < e; ++t) dsts[t] = dst + static_cast<size_t>(missing[t]) * share_len;
-        auto launch = [c, e](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
-            rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
-            set_patterns(c, 1, c->d_onepat.p, a);
-            a.stripe_desc = first_stripe_desc(c, c->d_onepat.p);  // e outputs, not m
-            return rsmi::launch_matmul(a, e, st);
-        };
-        err = c->pipe->run(srcs.data(), k, dsts.data(), e, share_len, launch);
-    }
-    // present data shares are copied as they are (Rebuild's output callback)
-    for (int i = 0; i < k; ++i)
-        if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * share_len, by_id[i], share_len);
-    return hip_status(err);
+    if (distinct > k) return correct_decode(c, present, by_id, share_len, dst);
+    return rebuild_into(c, present, by_id, share_len, dst);
 }
 
 void* rs_pinned_alloc(size_t bytes) {

@@ -29,6 +29,7 @@ RS_ESHARE_LEN = -7
 RS_EINVAL = -8
 RS_EDEVICE = -9
 RS_ENOMEM = -10
+RS_ETOO_MANY_ERRORS = -16
 
 # Every symbol include/rsmi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (

@@ -48,6 +48,10 @@ def lib() -> ctypes.CDLL:
         L.orc_encode.argtypes = [vp, i32, i32, vp, sz, vp]
         L.orc_decode.restype = i32
         L.orc_decode.argtypes = [vp, i32, i32, vp, vp, i32, sz, vp]
+        L.orc_decode_correct.restype = i32
+        L.orc_decode_correct.argtypes = [vp, i32, i32, vp, vp, i32, sz, vp]
+        L.orc_bw_column.restype = i32
+        L.orc_bw_column.argtypes = [vp, i32, i32, vp, vp, i32, vp]
         L.orc_invert.restype = i32
         L.orc_invert.argtypes = [vp, i32]
         L.orc_addmul.restype = None
@@ -104,6 +108,19 @@ def decode(enc: np.ndarray, k: int, n: int, shares: Sequence[Tuple[int, bytes]])
     dst = np.zeros(max(k * S, 1), dtype=np.uint8)
     rc = lib().orc_decode(_p(np.ascontiguousarray(enc)), k, n, ctypes.addressof(nums),
                           ctypes.addressof(ptrs), cnt, S, _p(dst))
+    return rc, dst[:k * S].tobytes()
+
+
+def decode_correct(enc: np.ndarray, k: int, n: int, shares: Sequence[Tuple[int, bytes]]) -> Tuple[int, bytes]:
+    """(*FEC).Decode with Correct (Berlekamp-Welch) for more than k shares."""
+    cnt = len(shares)
+    S = len(shares[0][1]) if cnt else 0
+    nums = (ctypes.c_int * max(cnt, 1))(*[s[0] for s in shares])
+    keep = [np.frombuffer(bytes(s[1]), dtype=np.uint8).copy() for s in shares]
+    ptrs = (ctypes.c_void_p * max(cnt, 1))(*[_p(b) if len(b) else None for b in keep])
+    dst = np.zeros(max(k * S, 1), dtype=np.uint8)
+    rc = lib().orc_decode_correct(_p(np.ascontiguousarray(enc)), k, n, ctypes.addressof(nums),
+                                  ctypes.addressof(ptrs), cnt, S, _p(dst))
     return rc, dst[:k * S].tobytes()
 
 

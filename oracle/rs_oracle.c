@@ -395,6 +395,156 @@ int orc_encode_batch(const uint8_t *enc, int k, int n, const uint8_t *data, uint
     return ORC_OK;
 }
 
+/* ---------------- Correct / Berlekamp-Welch --------------------------- */
+/* Codeword symbol i of the systematic code is P(x_i) for the polynomial P
+ * (degree < k) through the data symbols, with x_0 = 0, x_i = 2^i: c = E.d =
+ * V.(V_t^-1 d).  BW: find Q (deg < k+t) and monic E (deg t) with
+ * Q(x_i) = y_i E(x_i) for all received i; then P = Q / E. */
+static uint8_t pt_of(int num) { return num == 0 ? 0 : g_exp[num % 255]; }
+
+static uint8_t gpow8(uint8_t x, int e) {
+    if (e == 0) return 1;
+    if (x == 0) return 0;
+    return g_exp[(g_log[x] * e) % 255];
+}
+
+/* Solves A (rows x cols+1 augmented, row-major) by Gaussian elimination; on
+ * success (consistent) writes one solution (free variables 0) to sol[cols]. */
+static int solve_aug(uint8_t *A, int rows, int cols, uint8_t *sol) {
+    const int w = cols + 1;
+    int *pivcol = malloc(sizeof(int) * (size_t)(rows > 0 ? rows : 1));
+    int rank = 0;
+    for (int c = 0; c < cols && rank < rows; c++) {
+        int p = -1;
+        for (int r = rank; r < rows; r++)
+            if (A[r * w + c]) { p = r; break; }
+        if (p < 0) continue;
+        if (p != rank)
+            for (int j = 0; j < w; j++) { uint8_t t = A[p * w + j]; A[p * w + j] = A[rank * w + j]; A[rank * w + j] = t; }
+        uint8_t inv = g_inv[A[rank * w + c]];
+        for (int j = 0; j < w; j++) A[rank * w + j] = g_mul[inv][A[rank * w + j]];
+        for (int r = 0; r < rows; r++) {
+            if (r == rank || !A[r * w + c]) continue;
+            uint8_t f = A[r * w + c];
+            for (int j = 0; j < w; j++) A[r * w + j] ^= g_mul[f][A[rank * w + j]];
+        }
+        pivcol[rank++] = c;
+    }
+    for (int r = rank; r < rows; r++)
+        if (A[r * w + cols]) { free(pivcol); return 0; } /* inconsistent */
+    memset(sol, 0, (size_t)cols);
+    for (int r = 0; r < rank; r++) sol[pivcol[r]] = A[r * w + cols];
+    free(pivcol);
+    return 1;
+}
+
+int orc_bw_column(const uint8_t *enc, int k, int n, const int *nums, const uint8_t *ys, int r,
+                  uint8_t *out) {
+    (void)enc;
+    gf_ready();
+    const int emax = (r - k) / 2;
+    if (emax <= 0) return ORC_ENOT_ENOUGH;
+    for (int t = 1; t <= emax; t++) {
+        const int nq = k + t, cols = nq + t;
+        uint8_t *A = calloc((size_t)r * (cols + 1), 1), *u = calloc((size_t)cols, 1);
+        for (int i = 0; i < r; i++) {
+            const uint8_t x = pt_of(nums[i]), y = ys[i];
+            uint8_t *row = A + (size_t)i * (cols + 1);
+            for (int j = 0; j < nq; j++) row[j] = gpow8(x, j);
+            for (int l = 0; l < t; l++) row[nq + l] = g_mul[y][gpow8(x, l)];
+            row[cols] = g_mul[y][gpow8(x, t)];
+        }
+        int ok = solve_aug(A, r, cols, u);
+        if (ok) {
+            /* Q(x) = sum q_j x^j (q = u[0..nq)), E(x) = x^t + sum e_l x^l */
+            uint8_t *q = malloc((size_t)nq), *e = malloc((size_t)t + 1);
+            memcpy(q, u, (size_t)nq);
+            for (int l = 0; l < t; l++) e[l] = u[nq + l];
+            e[t] = 1;
+            /* P = Q / E (long division, E monic) */
+            uint8_t *pp = calloc((size_t)k, 1);
+            for (int d = nq - 1; d >= t; d--) {
+                const uint8_t c = q[d];
+                pp[d - t] = c;
+                if (c)
+                    for (int l = 0; l <= t; l++) q[d - t + l] ^= g_mul[c][e[l]];
+            }
+            for (int d = 0; d < t; d++) if (q[d]) ok = 0; /* remainder */
+            if (ok) {
+                int bad = 0;
+                for (int i = 0; i < r; i++) {
+                    uint8_t x = pt_of(nums[i]), v = 0;
+                    for (int d = k - 1; d >= 0; d--) v = g_mul[v][x] ^ pp[d];
+                    if (v != ys[i]) bad++;
+                }
+                if (bad > t) ok = 0;
+                else {
+                    for (int i = 0; i < n; i++) {
+                        uint8_t x = pt_of(i), v = 0;
+                        for (int d = k - 1; d >= 0; d--) v = g_mul[v][x] ^ pp[d];
+                        out[i] = v;
+                    }
+                    free(q); free(e); free(pp); free(A); free(u);
+                    return bad;
+                }
+            }
+            free(q); free(e); free(pp);
+        }
+        free(A);
+        free(u);
+    }
+    return ORC_ETOO_MANY;
+}
+
+int orc_decode_correct(const uint8_t *enc, int k, int n, int *numbers, const uint8_t **shares,
+                       int cnt, size_t S, uint8_t *dst) {
+    gf_ready();
+    if (cnt < k) return ORC_ENOT_ENOUGH;
+    for (int i = 0; i < cnt; i++)
+        if (numbers[i] < 0 || numbers[i] >= n) return ORC_EBAD_ID;
+    /* sort by number */
+    for (int i = 1; i < cnt; i++) {
+        int num = numbers[i];
+        const uint8_t *sh = shares[i];
+        int j = i - 1;
+        while (j >= 0 && numbers[j] > num) { numbers[j + 1] = numbers[j]; shares[j + 1] = shares[j]; j--; }
+        numbers[j + 1] = num;
+        shares[j + 1] = sh;
+    }
+    /* private copies, corrected in place (infectious mutates the shares) */
+    uint8_t **cp = malloc(sizeof(uint8_t *) * (size_t)cnt);
+    for (int i = 0; i < cnt; i++) { cp[i] = malloc(S ? S : 1); memcpy(cp[i], shares[i], S); }
+    int rc = ORC_OK;
+    if (cnt > k) {
+        /* consistency: every share must equal enc[num] . data, data being
+         * the codeword through the first k shares */
+        int *kn = malloc(sizeof(int) * (size_t)k);
+        const uint8_t **kp = malloc(sizeof(*kp) * (size_t)k);
+        uint8_t *d = malloc((size_t)k * (S ? S : 1));
+        for (int i = 0; i < k; i++) { kn[i] = numbers[i]; kp[i] = cp[i]; }
+        rc = orc_decode(enc, k, n, kn, kp, k, S, d);
+        uint8_t *ys = malloc((size_t)cnt), *outv = malloc((size_t)n);
+        for (size_t col = 0; col < S && rc == ORC_OK; col++) {
+            int consistent = 1;
+            for (int i = k; i < cnt && consistent; i++) {
+                uint8_t v = 0;
+                for (int j = 0; j < k; j++) v ^= g_mul[enc[numbers[i] * k + j]][d[(size_t)j * S + col]];
+                if (v != cp[i][col]) consistent = 0;
+            }
+            if (consistent) continue;
+            for (int i = 0; i < cnt; i++) ys[i] = cp[i][col];
+            int c = orc_bw_column(enc, k, n, numbers, ys, cnt, outv);
+            if (c < 0) { rc = c; break; }
+            for (int i = 0; i < cnt; i++) cp[i][col] = outv[numbers[i]];
+        }
+        free(kn); free(kp); free(d); free(ys); free(outv);
+    }
+    if (rc == ORC_OK) rc = orc_decode(enc, k, n, numbers, (const uint8_t **)cp, cnt, S, dst);
+    for (int i = 0; i < cnt; i++) free(cp[i]);
+    free(cp);
+    return rc;
+}
+
 /* ---------------- batched reconstruct (CPU baseline) ------------------ */
 typedef struct {
     const uint8_t *enc, *erased;

@@ -31,6 +31,7 @@ enum {
     ORC_EBAD_ID = -4,          /* "invalid share id"                       */
     ORC_ESINGULAR = -5,        /* "singular matrix"                        */
     ORC_ENOSHARES = -6,        /* "must specify at least one share"        */
+    ORC_ETOO_MANY = -7,        /* TooManyErrors (Berlekamp-Welch)          */
 };
 
 /* GF(2^8), poly 0x11D, generator 2. */
@@ -57,6 +58,22 @@ int orc_encode(const uint8_t *enc, int k, int n, const uint8_t *input,
 int orc_decode(const uint8_t *enc, int k, int n, int *numbers,
                const uint8_t **shares, int cnt, size_t share_len,
                uint8_t *dst);
+
+/* Berlekamp-Welch correction of one byte column (infectious Correct /
+ * berlekampWelch, the Decode path for more than k shares): nums[r] share
+ * numbers, ys[r] received bytes.  Finds the nearest codeword within
+ * floor((r-k)/2) errors (trying 1, 2, ... errors) and writes its value at
+ * every share number 0..n-1 to out[n].  Returns the number of corrected
+ * symbols, or ORC_ETOO_MANY when none exists (ORC_ENOT_ENOUGH if r - k < 2).
+ * Restates the result of infectious's algorithm (a unique nearest codeword);
+ * its behaviour for columns it cannot solve is not pinned. */
+int orc_bw_column(const uint8_t *enc, int k, int n, const int *nums, const uint8_t *ys, int r,
+                  uint8_t *out);
+
+/* Decode with correction: Correct (syndrome + Berlekamp-Welch on every
+ * inconsistent column) then Rebuild, for cnt >= k distinct shares. */
+int orc_decode_correct(const uint8_t *enc, int k, int n, int *numbers, const uint8_t **shares,
+                       int cnt, size_t share_len, uint8_t *dst);
 
 /* infectious invertMatrix (Gauss-Jordan over GF(2^8)), in place. */
 int orc_invert(uint8_t *a, int k);

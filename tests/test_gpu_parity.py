@@ -355,3 +355,64 @@ def test_reconstruct_wide_code_unique_patterns():
     f.sync()
     assert f.pattern_count() == len({r.tobytes() for r in er})
     assert torch.equal(data, d0) and torch.equal(parity, p0)
+
+
+# --------------------------------------- Decode with Correct (> k shares) ----
+def _corrupt(sh, ids, rng, cols=None):
+    out = [bytearray(x) for x in sh]
+    for i in ids:
+        if cols is None:
+            out[i] = bytearray(rng.integers(0, 256, len(out[i]), dtype=np.uint8).tobytes())
+        else:
+            for c in cols:
+                out[i][c] ^= int(rng.integers(1, 256))
+    return [bytes(x) for x in out]
+
+
+@pytest.mark.parametrize("k,n,bad", [(10, 14, [3]), (10, 14, [12]), (10, 14, [0, 13]),
+                                     (4, 6, [1]), (64, 80, [0, 5, 17, 63, 64, 70, 71, 79])])
+def test_decode_corrects_whole_share_errors(k, n, bad):
+    S = 777
+    data, sh = _shards(k, n, S, k * 7 + n)
+    rng = np.random.default_rng(len(bad))
+    cor = _corrupt(sh, bad, rng)
+    shares = [rsmi.Share(i, cor[i]) for i in range(n)][::-1]
+    assert fec(k, n).Decode(None, shares) == data
+    rc, ref = oracle.decode_correct(oracle.fec_matrix(k, n), k, n, [(i, cor[i]) for i in range(n)])
+    assert rc == 0 and ref == data
+
+
+def test_decode_corrects_scattered_column_errors():
+    """Different shares are bad in different columns (each column within the
+    correction radius): the located-erasure pass leaves columns that need
+    per-column Berlekamp-Welch."""
+    k, n, S = 10, 14, 4096
+    data, sh = _shards(k, n, S, 99)
+    rng = np.random.default_rng(5)
+    cor = [bytearray(x) for x in sh]
+    for c in range(0, S, 7):
+        for i in rng.choice(n, size=int(rng.integers(1, 3)), replace=False):
+            cor[i][c] ^= int(rng.integers(1, 256))
+    cor = [bytes(x) for x in cor]
+    assert fec(k, n).Decode(None, [rsmi.Share(i, cor[i]) for i in range(n)]) == data
+    rc, ref = oracle.decode_correct(oracle.fec_matrix(k, n), k, n, [(i, cor[i]) for i in range(n)])
+    assert rc == 0 and ref == data
+
+
+def test_decode_correct_error_cases():
+    k, n, S = 10, 14, 256
+    data, sh = _shards(k, n, S, 123)
+    rng = np.random.default_rng(8)
+    f = fec(k, n)
+    cor = _corrupt(sh, [1, 6, 11], rng)  # 3 bad > floor(4/2)
+    with pytest.raises(rsmi.RSError) as ei:
+        f.Decode(None, [rsmi.Share(i, cor[i]) for i in range(n)])
+    assert ei.value.code == rsmi.RS_ETOO_MANY_ERRORS
+    rc, _ = oracle.decode_correct(oracle.fec_matrix(k, n), k, n, [(i, cor[i]) for i in range(n)])
+    assert rc == -7
+    cor = _corrupt(sh, [2], rng)  # k+1 shares: inconsistency found, nothing to correct with
+    with pytest.raises(rsmi.NotEnoughShares):
+        f.Decode(None, [rsmi.Share(i, cor[i]) for i in range(k + 1)])
+    # exactly k shares: no check, like infectious (the corruption passes)
+    got = f.Decode(None, [rsmi.Share(i, cor[i]) for i in range(k)])
+    assert got != data and got[2 * S:3 * S] == cor[2]

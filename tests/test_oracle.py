@@ -139,3 +139,19 @@ def test_batch_encode_matches_single():
         for s in range(stripes):
             ref = oracle.encode(E, k, n, data[s * k * S:(s + 1) * k * S].tobytes())
             assert par[s * (n - k) * S:(s + 1) * (n - k) * S].tobytes() == ref
+
+
+def test_oracle_berlekamp_welch():
+    k, n, S = 10, 14, 64
+    E = oracle.fec_matrix(k, n)
+    data = oracle.splitmix_bytes(k * S, 17).tobytes()
+    par = oracle.encode(E, k, n, data)
+    sh = [bytearray(data[i * S:(i + 1) * S]) for i in range(k)] + \
+         [bytearray(par[i * S:(i + 1) * S]) for i in range(n - k)]
+    sh[4] = bytearray(b"\xAA" * S)     # whole data share wrong
+    sh[13][5] ^= 0x11                  # one parity byte wrong
+    rc, out = oracle.decode_correct(E, k, n, [(i, bytes(sh[i])) for i in range(n)][::-1])
+    assert rc == 0 and out == data
+    sh[9] = bytearray(S)               # third bad share: beyond floor(4/2)
+    rc, _ = oracle.decode_correct(E, k, n, [(i, bytes(sh[i])) for i in range(n)])
+    assert rc == -7
