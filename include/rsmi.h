@@ -90,6 +90,19 @@ int rs_encode(rs_ctx *ctx, const uint8_t *input, size_t len, uint8_t *parity);
 int rs_decode(rs_ctx *ctx, int *numbers, const uint8_t **shares, int count,
               size_t share_len, uint8_t *dst);
 
+/* rs_decode_batch: receive-side batching -- Decode
+ * for `batch` messages of this code in one GPU pass.  Message b has
+ * counts[b] shares; their numbers / pointers are consecutive in numbers[] /
+ * shares[] (message b starts at sum(counts[0..b))), each share_len bytes;
+ * dsts[b] receives k * share_len bytes.  Per-message results go to
+ * status[b] (rs_decode's codes; each message's slice of numbers/shares is
+ * sorted in place).  Messages with more than k distinct shares take the
+ * rs_decode path (Correct); the rest are staged through pinned memory and
+ * regenerated by one rs_reconstruct_stripes launch.  Returns RS_OK if every
+ * message decoded, else the first failing status. */
+int rs_decode_batch(rs_ctx *ctx, int batch, const int *counts, int *numbers,
+                    const uint8_t **shares, size_t share_len, uint8_t **dsts, int *status);
+
 /* ---- device-resident batched API (many stripes per launch) ---------------
  * Stripe s, shard i lives at
  *     i <  k:  data   + s * data_stripe_stride   + i       * shard_pitch

@@ -56,6 +56,9 @@ public:
     hipError_t run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e, size_t S,
                    const ChunkLaunch& launch);
 
+    // Parallel pageable <-> pinned copies on the pipeline's worker pool.
+    void copy(const std::vector<CopyPool::Piece>& pieces) { pool_.run(pieces); }
+
     static constexpr int kSlots = 3;
 
 private:

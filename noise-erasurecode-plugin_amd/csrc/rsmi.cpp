@@ -145,6 +145,9 @@ struct rs_ctx {
     Staging st_stripe;   // stripe descriptors
     std::vector<uint32_t> scratch_pid, scratch_start;
 
+    // rs_decode_batch staging: pinned [batch][n][pitch] image and its device twin.
+    Staging st_batch;
+    DevBuf d_batch;
     // Host-buffer API: pinned staging pipeline (created on first use) and the
     // device copy of a decode call's one-pattern table.
     std::unique_ptr<rsmi::HostPipeline> pipe;
@@ -489,6 +492,10 @@ int correct_decode(rs_ctx* c, std::vector<uint8_t> present, const std::vector<co
 
 }  // namespace
 
+static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
+                              size_t pitch, size_t len, size_t stripes, const uint8_t* erased,
+                              hipStream_t s);
+
 extern "C" {
 
 const char* rs_strerror(int st) {
@@ -577,7 +584,8 @@ void rs_free(rs_ctx* c) {
         c->st_pat.destroy();
         c->st_stripe.destroy();
         c->st_one.destroy();
-        for (DevBuf* b : {&c->d_encpat, &c->d_stripe_pat, &c->d_work, &c->d_onepat, &c->d_gf})
+        c->st_batch.destroy();
+        for (DevBuf* b : {&c->d_encpat, &c->d_stripe_pat, &c->d_work, &c->d_onepat, &c->d_gf, &c->d_batch})
             b->release();
         for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt}) b->release();
         if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -679,7 +687,14 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    return reconstruct_locked(c, data, dss, parity, pss, pitch, len, stripes, erased,
+                              static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"
+
+static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss, size_t pitch,
+                              size_t len, size_t stripes, const uint8_t* erased, hipStream_t s) {
     if (c->pat_index.size() + stripes > (size_t(1) << 20)) reset_patterns(c);  // ids are 24-bit
     // Pattern of every stripe, then a counting sort by pattern: the launch
     // lists stripes grouped by pattern (see rs_kernels.hpp stripe_desc).
@@ -723,6 +738,7 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     a.stripe_desc = static_cast<const uint2*>(c->d_stripe_pat.p);
     return hip_status(rsmi::launch_matmul(a, max_e, s));
 }
+extern "C" {
 
 int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     if (!c) return RS_EINVAL;
@@ -786,6 +802,103 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (!g.ok) return RS_EDEVICE;
     if (distinct > k) return correct_decode(c, present, by_id, share_len, dst);
     return rebuild_into(c, present, by_id, share_len, dst);
+}
+
+int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const uint8_t** shares,
+                    size_t S, uint8_t** dsts, int* status) {
+    if (!c || batch < 0 || (batch && (!counts || !numbers || !shares || !dsts || !status)))
+        return RS_EINVAL;
+    const int k = c->k, n = c->n;
+    // 1. validate + sort each message (rs_decode semantics); pick the ones
+    //    the batched path handles (exactly... at most k distinct shares is
+    //    impossible past validation, so: distinct == k, plus any count with
+    //    duplicates collapsing to k).
+    std::vector<size_t> first(batch + 1, 0);
+    for (int b = 0; b < batch; ++b) first[b + 1] = first[b] + static_cast<size_t>(std::max(counts[b], 0));
+    std::vector<int> fast;  // messages for the batched launch
+    std::vector<std::vector<const uint8_t*>> by(batch);
+    int rc = RS_OK;
+    for (int b = 0; b < batch; ++b) {
+        int* nb = numbers + first[b];
+        const uint8_t** sb = shares + first[b];
+        const int cnt = counts[b];
+        status[b] = RS_OK;
+        if (cnt < k) status[b] = RS_ENOT_ENOUGH;
+        for (int i = 0; i < cnt && status[b] == RS_OK; ++i)
+            if (nb[i] < 0 || nb[i] >= n) status[b] = RS_EBAD_SHARE_ID;
+        if (status[b] != RS_OK) {
+            if (rc == RS_OK) rc = status[b];
+            continue;
+        }
+        std::vector<int> order(cnt);
+        for (int i = 0; i < cnt; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return nb[x] < nb[y]; });
+        std::vector<int> nums(cnt);
+        std::vector<const uint8_t*> ptrs(cnt);
+        for (int i = 0; i < cnt; ++i) {
+            nums[i] = nb[order[i]];
+            ptrs[i] = sb[order[i]];
+        }
+        std::copy(nums.begin(), nums.end(), nb);
+        std::copy(ptrs.begin(), ptrs.end(), sb);
+        by[b].assign(n, nullptr);
+        int distinct = 0;
+        for (int i = 0; i < cnt; ++i)
+            if (!by[b][nums[i]]) {
+                by[b][nums[i]] = ptrs[i];
+                ++distinct;
+            }
+        if (distinct < k) {
+            status[b] = RS_ESINGULAR;
+            if (rc == RS_OK) rc = status[b];
+        } else if (distinct > k) {
+            status[b] = 1;  // Correct path, below
+        } else if (S > 0) {
+            fast.push_back(b);
+        }
+    }
+    // 2. messages needing Correct: one by one
+    for (int b = 0; b < batch; ++b) {
+        if (status[b] != 1) continue;
+        status[b] = rs_decode(c, numbers + first[b], shares + first[b], counts[b], S, dsts[b]);
+        if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
+    }
+    if (fast.empty()) return rc;
+    // 3. the rest: one reconstruct launch over [batch][n][pitch]
+    const size_t pitch = round_up(S, 256), stripe = pitch * static_cast<size_t>(n);
+    const size_t B = fast.size();
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
+    if (!c->st_batch.acquire(B * stripe) || !c->d_batch.reserve(B * stripe)) return RS_ENOMEM;
+    uint8_t* h = static_cast<uint8_t*>(c->st_batch.p);
+    std::vector<uint8_t> erased(B * static_cast<size_t>(n), 0);
+    std::vector<rsmi::CopyPool::Piece> in;
+    for (size_t j = 0; j < B; ++j)
+        for (int i = 0; i < n; ++i) {
+            const uint8_t* p = by[fast[j]][i];
+            if (p)
+                in.push_back({h + j * stripe + static_cast<size_t>(i) * pitch, p, S});
+            else
+                erased[j * n + i] = 1;
+        }
+    c->pipe->copy(in);
+    uint8_t* d = static_cast<uint8_t*>(c->d_batch.p);
+    hipStream_t s = c->stream;
+    if (hipMemcpyAsync(d, h, B * stripe, hipMemcpyHostToDevice, s) != hipSuccess) return RS_EDEVICE;
+    const int st = reconstruct_locked(c, d, stripe, d + pitch * k, stripe, pitch, S, B, erased.data(), s);
+    if (st != RS_OK) return st;
+    if (hipMemcpy2DAsync(h, stripe, d, stripe, pitch * k, B, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return RS_EDEVICE;
+    c->st_batch.release_after(s);
+    std::vector<rsmi::CopyPool::Piece> out;
+    for (size_t j = 0; j < B; ++j)
+        for (int i = 0; i < k; ++i)
+            out.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, h + j * stripe + i * pitch, S});
+    c->pipe->copy(out);
+    return rc;
 }
 
 void* rs_pinned_alloc(size_t bytes) {

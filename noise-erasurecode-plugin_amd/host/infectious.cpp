@@ -79,4 +79,40 @@ Status FEC::Decode(std::vector<uint8_t>* dst, std::vector<Share>& shares) {
     return Status::Ok();
 }
 
+Status FEC::DecodeBatch(std::vector<std::vector<Share>>& msgs, std::vector<std::vector<uint8_t>>* out,
+                        std::vector<Status>* st) {
+    const int B = static_cast<int>(msgs.size());
+    out->assign(B, {});
+    st->assign(B, Status::Ok());
+    if (B == 0) return Status::Ok();
+    const size_t S = msgs[0].empty() ? 0 : msgs[0][0].Data.size();
+    std::vector<int> counts(B), nums;
+    std::vector<const uint8_t*> ptrs;
+    for (int b = 0; b < B; ++b) {
+        counts[b] = static_cast<int>(msgs[b].size());
+        for (const Share& s : msgs[b]) {
+            if (s.Data.size() != S) return from(RS_ESHARE_LEN, "DecodeBatch");
+            nums.push_back(s.Number);
+            ptrs.push_back(s.Data.data());
+        }
+    }
+    std::vector<uint8_t*> dsts(B);
+    for (int b = 0; b < B; ++b) {
+        (*out)[b].resize(static_cast<size_t>(k_) * S);
+        dsts[b] = (*out)[b].data();
+    }
+    std::vector<int> codes(B, 0);
+    const int rc = rs_decode_batch(ctx_, B, counts.data(), nums.data(), ptrs.data(), S, dsts.data(),
+                                   codes.data());
+    for (int b = 0; b < B; ++b) {
+        if (codes[b] != RS_OK) {
+            (*st)[b] = from(codes[b], "Decode");
+            (*out)[b].clear();
+        }
+        std::stable_sort(msgs[b].begin(), msgs[b].end(),
+                         [](const Share& x, const Share& y) { return x.Number < y.Number; });
+    }
+    return rc == RS_OK ? Status::Ok() : from(rc, "DecodeBatch");
+}
+
 }  // namespace rsmi_host

@@ -58,6 +58,10 @@ public:
                   const std::function<void(const ShareView&)>& output);
     // Sorts `shares` by Number in place; *dst receives k * len(share) bytes.
     Status Decode(std::vector<uint8_t>* dst, std::vector<Share>& shares);
+    // Decode of many messages (same share length) in one GPU pass
+    // (rs_decode_batch); (*out)[b] / (*st)[b] per message.
+    Status DecodeBatch(std::vector<std::vector<Share>>& msgs, std::vector<std::vector<uint8_t>>* out,
+                       std::vector<Status>* st);
 
 private:
     friend Status NewFEC(int k, int n, std::shared_ptr<FEC>* out);

@@ -59,6 +59,16 @@ PYBIND11_MODULE(_rsmi_host, m) {
                  check(f.Encode(reinterpret_cast<const uint8_t*>(s.data()), s.size(),
                                 [&](const ShareView& v) { output(v.DeepCopy()); }));
              })
+        .def("DecodeBatch",
+             [](FEC& f, std::vector<std::vector<Share>> msgs) {
+                 std::vector<std::vector<uint8_t>> outs;
+                 std::vector<Status> st;
+                 f.DecodeBatch(msgs, &outs, &st);
+                 py::list res;
+                 for (size_t b = 0; b < outs.size(); ++b)
+                     res.append(st[b].ok() ? py::object(to_bytes(outs[b])) : py::object(py::none()));
+                 return res;
+             })
         .def("Decode", [](FEC& f, py::object /*dst*/, std::vector<Share>& shares) {
             std::vector<uint8_t> out;
             check(f.Decode(&out, shares));
@@ -121,6 +131,18 @@ PYBIND11_MODULE(_rsmi_host, m) {
                  ReceiveEvent ev;
                  check(p.Receive(sender, msg, &ev));
                  return ev;
+             })
+        .def("ReceiveBatch",
+             [](ShardPlugin& p, const std::vector<std::pair<PeerID, Shard>>& msgs) {
+                 std::vector<ReceiveEvent> evs;
+                 std::vector<Status> sts;
+                 {
+                     py::gil_scoped_release nogil;
+                     p.ReceiveBatch(msgs, &evs, &sts);
+                 }
+                 std::vector<int> codes;
+                 for (const Status& s : sts) codes.push_back(s.code);
+                 return py::make_tuple(evs, codes);
              })
         .def("prepareShards",
              [](ShardPlugin& p, const PeerID& self, py::object input) {

@@ -2,6 +2,8 @@
 #include "shard_plugin.hpp"
 
 #include <algorithm>
+#include <map>
+#include <tuple>
 
 #include "../../include/rsmi.h"
 #include "../../include/rsmi_wire.h"
@@ -193,6 +195,104 @@ Status ShardPlugin::Receive(const PeerID& sender, const Shard& msg, ReceiveEvent
     if (pool.size() == msg.TotalShards)  // main.go:96-98
         return Status::Err(RS_ESINGULAR, "Could not put together the message due to corruption");
     return Status::Ok();
+}
+
+void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs,
+                               std::vector<ReceiveEvent>* evs, std::vector<Status>* sts) {
+    evs->assign(msgs.size(), ReceiveEvent{});
+    sts->assign(msgs.size(), Status::Ok());
+    struct Job {
+        size_t msg;
+        std::string key;
+        std::vector<Share> pool;
+    };
+    std::vector<size_t> pending(msgs.size());
+    for (size_t i = 0; i < msgs.size(); ++i) pending[i] = i;
+    while (!pending.empty()) {
+        std::vector<size_t> deferred;
+        std::vector<Job> jobs;
+        std::unordered_map<std::string, bool> busy;  // key has a decode this phase
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (size_t i : pending) {
+                const Shard& msg = msgs[i].second;
+                ReceiveEvent& e = (*evs)[i];
+                const std::string key = HexString(msg.FileSignature);
+                if (busy.count(key)) {
+                    deferred.push_back(i);
+                    continue;
+                }
+                auto it = shards_.find(key);
+                if (it == shards_.end()) {
+                    shards_[key].push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+                    e.pooled = true;
+                    continue;
+                }
+                std::vector<Share>& p = it->second;
+                const int64_t len = static_cast<int64_t>(p.size());
+                if (len < static_cast<int64_t>(msg.MinimumNeededShards)) {
+                    p.push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+                    e.pooled = true;
+                    continue;
+                }
+                if (!(len >= static_cast<int64_t>(msg.MinimumNeededShards) &&
+                      len <= static_cast<int64_t>(msg.TotalShards))) {
+                    (*sts)[i] = Status::Err(RS_EINVAL, "Shards mempool is larger than maximum size");
+                    continue;
+                }
+                busy[key] = true;
+                jobs.push_back(Job{i, key, p});
+            }
+        }
+        // Decode the phase's pools, grouped by (k, n, share length).
+        std::map<std::tuple<uint64_t, uint64_t, size_t>, std::vector<size_t>> groups;
+        for (size_t j = 0; j < jobs.size(); ++j) {
+            const Shard& m = msgs[jobs[j].msg].second;
+            const size_t S = jobs[j].pool.empty() ? 0 : jobs[j].pool[0].Data.size();
+            groups[{m.MinimumNeededShards, m.TotalShards, S}].push_back(j);
+        }
+        for (auto& g : groups) {
+            std::vector<size_t>& ids = g.second;
+            for (size_t j : ids) (*evs)[jobs[j].msg].decoded = true;
+            std::shared_ptr<FEC> f;
+            Status fs = CachedFEC(static_cast<int>(std::get<0>(g.first)),
+                                  static_cast<int>(std::get<1>(g.first)), &f);
+            std::vector<std::vector<Share>> pools;
+            std::vector<std::vector<uint8_t>> outs;
+            std::vector<Status> st;
+            bool uniform = true;  // a pool with mixed share lengths goes alone
+            for (size_t j : ids)
+                for (const Share& s : jobs[j].pool) uniform &= s.Data.size() == std::get<2>(g.first);
+            if (fs.ok() && uniform) {
+                for (size_t j : ids) pools.push_back(jobs[j].pool);
+                f->DecodeBatch(pools, &outs, &st);
+            } else {
+                for (size_t j : ids) {
+                    std::vector<uint8_t> o;
+                    Status s1 = fs.ok() ? f->Decode(&o, jobs[j].pool) : fs;
+                    outs.push_back(std::move(o));
+                    st.push_back(s1);
+                }
+            }
+            for (size_t q = 0; q < ids.size(); ++q) {
+                const Job& jb = jobs[ids[q]];
+                ReceiveEvent& e = (*evs)[jb.msg];
+                const Shard& msg = msgs[jb.msg].second;
+                e.decode_status = st[q];
+                if (st[q].ok()) e.message = std::move(outs[q]);
+                e.verified = st[q].ok() && verify_ &&
+                             verify_(serializeMessage(msgs[jb.msg].first, e.message), msg.FileSignature);
+                if (e.verified) {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    shards_.erase(jb.key);
+                } else if (jb.pool.size() == msg.TotalShards) {
+                    (*sts)[jb.msg] = Status::Err(RS_ESINGULAR,
+                                                 "Could not put together the message due to corruption");
+                }
+            }
+        }
+        pending.swap(deferred);
+    }
 }
 
 }  // namespace rsmi_host

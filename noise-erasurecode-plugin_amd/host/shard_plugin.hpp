@@ -84,6 +84,15 @@ public:
     // more than TotalShards is an error.
     Status Receive(const PeerID& sender, const Shard& msg, ReceiveEvent* ev = nullptr);
 
+    // Receive for a batch of arrivals (receive-side batching, SURVEY.md §8f
+    // rank 3): the same pooling rules and per-key order as calling Receive on
+    // each message in turn, but every pool that triggers in a phase is
+    // decoded in one GPU pass (FEC::DecodeBatch per (k, n, share length)).
+    // Arrivals for a key whose decode is in flight wait for the next phase.
+    // (*evs)[i] / (*sts)[i] correspond to msgs[i].
+    void ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs,
+                      std::vector<ReceiveEvent>* evs, std::vector<Status>* sts);
+
     // main.go:201-210 with net.Broadcast replaced by `broadcast`.
     Status ShardAndBroadcast(const PeerID& self, const std::vector<uint8_t>* input,
                              const std::function<void(const Shard&)>& broadcast);

@@ -34,7 +34,7 @@ RS_ETOO_MANY_ERRORS = -16
 # Every symbol include/rsmi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (
     "rs_new", "rs_new_on_device", "rs_free", "rs_k", "rs_n", "rs_device",
-    "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode",
+    "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode", "rs_decode_batch",
     "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_prepare_patterns",
     "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
@@ -79,6 +79,8 @@ def _lib() -> ctypes.CDLL:
             "rs_strerror": (ctypes.c_char_p, [i32]),
             "rs_encode": (i32, [vp, vp, sz, vp]),
             "rs_decode": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(vp), i32, sz, vp]),
+            "rs_decode_batch": (i32, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                      ctypes.POINTER(vp), sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
             "rs_encode_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp]),
             "rs_reconstruct_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp, vp]),
             "rs_pattern_count": (i32, [vp]),
@@ -219,6 +221,28 @@ class FEC:
             dst[:len(out)] = out
             return bytes(dst[:len(out)])
         return bytes(out)
+
+    def DecodeBatch(self, messages: List[List[Share]]):
+        """rs_decode_batch: decode many messages in one GPU pass.  Returns
+        (outputs, statuses); outputs[b] is None where statuses[b] != 0."""
+        B = len(messages)
+        S = len(messages[0][0].Data) if B and messages[0] else 0
+        counts = (ctypes.c_int * max(B, 1))(*[len(msg) for msg in messages])
+        flat = [s for msg in messages for s in msg]
+        for s in flat:
+            if len(s.Data) != S:
+                raise RSError(RS_ESHARE_LEN, "DecodeBatch")
+        nums = (ctypes.c_int * max(len(flat), 1))(*[s.Number for s in flat])
+        keep = [bytes(s.Data) for s in flat]
+        ptrs = (ctypes.c_void_p * max(len(flat), 1))(
+            *[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value for b in keep])
+        outs = [bytearray(max(self.k * S, 1)) for _ in range(B)]
+        outp = (ctypes.c_void_p * max(B, 1))(
+            *[ctypes.addressof((ctypes.c_char * max(len(o), 1)).from_buffer(o)) for o in outs])
+        st = (ctypes.c_int * max(B, 1))()
+        _lib().rs_decode_batch(self._h, B, counts, nums, ptrs, S, outp, st)
+        return ([bytes(o[:self.k * S]) if st[b] == RS_OK else None for b, o in enumerate(outs)],
+                [st[b] for b in range(B)])
 
     # -- device-resident batched API -------------------------------------------
     def encode_stripes(self, data_ptr: int, data_stride: int, parity_ptr: int,

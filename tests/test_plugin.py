@@ -177,3 +177,59 @@ def test_host_fec_api():
     got, sorted_shares = f.Decode(None, [shares[i] for i in (13, 1, 9, 2, 12, 3, 11, 7)])
     assert got == b"hello, world! __"
     assert [s.Number for s in sorted_shares] == sorted([13, 1, 9, 2, 12, 3, 11, 7])
+
+
+def test_decode_batch_matches_decode():
+    import rsmi
+    k, n, S = 10, 14, 1000
+    f = rsmi.NewFEC(k, n)
+    E = oracle.fec_matrix(k, n)
+    rng = np.random.default_rng(77)
+    msgs, want = [], []
+    for b in range(40):
+        data = oracle.splitmix_bytes(k * S, 500 + b).tobytes()
+        par = oracle.encode(E, k, n, data)
+        sh = [data[i * S:(i + 1) * S] for i in range(k)] + [par[i * S:(i + 1) * S] for i in range(n - k)]
+        cnt = k if b % 5 else k + 2                  # every 5th message takes the Correct path
+        keep = rng.choice(n, size=cnt, replace=False).tolist()
+        if b % 10 == 0:                              # ... and one of its shares is corrupted
+            sh[keep[0]] = bytes(len(sh[keep[0]]))
+        msgs.append([rsmi.Share(i, sh[i]) for i in keep])
+        want.append(data)
+    msgs.append([rsmi.Share(0, b"x" * S)] * k)     # duplicate numbers: singular
+    outs, st = f.DecodeBatch(msgs)
+    assert outs[:-1] == want and all(s == 0 for s in st[:-1])
+    assert st[-1] == rsmi.RS_ESINGULAR and outs[-1] is None
+    # the C++ host layer's FEC::DecodeBatch gives the same
+    hf = h.NewFEC(k, n)
+    got = hf.DecodeBatch([[h.Share(s.Number, bytes(s.Data)) for s in m] for m in msgs[:-1]])
+    assert got == want
+
+
+def test_receive_batch_equals_sequential_receive():
+    k, n = 10, 14
+    rng = np.random.default_rng(5)
+    senders = [h.PeerID(f"tcp://peer{i}:3000", bytes([i]) * 32) for i in range(6)]
+    arrivals = []
+    expect = {}
+    for mnum in range(30):
+        snd = senders[mnum % len(senders)]
+        msg = oracle.splitmix_bytes(10 * (50 + mnum), mnum).tobytes()
+        shards = plugin(k, n).prepareShards(snd, msg)
+        lost = rng.choice(n, size=int(rng.integers(0, 4)), replace=False)
+        for i in [i for i in range(n) if i not in lost]:
+            arrivals.append((snd, shards[i]))
+        expect[shards[0].FileSignature] = msg
+    order = rng.permutation(len(arrivals))
+    arrivals = [arrivals[i] for i in order]
+    seq = plugin(k, n)
+    seq_ev = [seq.Receive(s, m) for s, m in arrivals]
+    bat = plugin(k, n)
+    bat_ev, codes = bat.ReceiveBatch(arrivals)
+    assert all(c == 0 for c in codes)
+    for a, b, (_, m) in zip(seq_ev, bat_ev, arrivals):
+        assert (a.pooled, a.decoded, a.verified) == (b.pooled, b.decoded, b.verified)
+        assert a.message == b.message
+        if b.verified:
+            assert b.message == expect[m.FileSignature]
+    assert sum(e.verified for e in bat_ev) == len(expect)
