@@ -78,14 +78,22 @@ typedef __attribute__((address_space(1))) const u32x4 GlobalCU4;
 typedef __attribute__((address_space(1))) u32x4 GlobalU4;
 
 // Global (not flat) 16-byte load/store: flat ops would count on lgkmcnt too
-// and serialise against the LDS table reads.
+// and serialise against the LDS table reads.  NT sets the non-temporal cache
+// policy bit: every shard byte is touched exactly once per launch, and on
+// MI355X nt loads + nt stores raise the 10-read/4-write movement ceiling from
+// 5.84 to 6.26 TB/s (profiles/r01_membench_cachepolicy.log).
+template <bool NT>
 __device__ __forceinline__ uint4 gload16(const uint8_t* p) {
-    const u32x4 v = *(GlobalCU4*)(p);
+    u32x4 v;
+    if constexpr (NT) v = __builtin_nontemporal_load((GlobalCU4*)(p));
+    else v = *(GlobalCU4*)(p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+template <bool NT>
 __device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
     u32x4 w = {v.x, v.y, v.z, v.w};
-    *(GlobalU4*)(p) = w;
+    if constexpr (NT) __builtin_nontemporal_store(w, (GlobalU4*)(p));
+    else *(GlobalU4*)(p) = w;
 }
 
 // Wave-uniform 64-bit value into SGPRs.
@@ -133,7 +141,7 @@ __device__ __forceinline__ void step_fence(uint32_t (&acc)[kRowsPerStep][4]) {
 
 // One block codes a chunk of 16-byte columns of one stripe for one group of
 // MG output rows.  LDS: [k][MG/4][20] table dwords | k survivor pointers.
-template <int K, int MG, int BT>
+template <int K, int MG, int BT, bool NT>
 __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     static_assert(MG % kRowsPerStep == 0, "MG must be a multiple of 4");
     constexpr int TG = MG / kRowsPerStep;                 // sub-steps per survivor
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     const uint32_t off0 = (col0 <= last ? col0 : last) * 16u;
     if constexpr (kRegPtrs) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) xpre[j] = gload16(sp[j] + off0);
+        for (int j = 0; j < K; ++j) xpre[j] = gload16<NT>(sp[j] + off0);
     }
     // Output pointers are only needed at store time.  Rows are padded to 16
     // ids, so whole 4-id groups load unconditionally (s_load_dwordx4); rows
@@ -248,7 +256,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
 #pragma unroll
                 for (int q = 0; q < JB; ++q) {
                     if (K == 0 && jb + q >= k) break;
-                    x[q] = gload16(uniform_ptr(sptr[jb + q]) + off);
+                    x[q] = gload16<NT>(uniform_ptr(sptr[jb + q]) + off);
                 }
             }
             uint32_t TA[kStepWords], TB[kStepWords];
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
             if (it + 1 < a.iters && colbase + BT < a.ncols16) {
                 const uint32_t noff = (ncol <= last ? ncol : last) * 16u;
 #pragma unroll
-                for (int j = 0; j < K; ++j) xpre[j] = gload16(sp[j] + noff);
+                for (int j = 0; j < K; ++j) xpre[j] = gload16<NT>(sp[j] + noff);
             }
         }
 #pragma unroll
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
             for (int r = 0; r < kRowsPerStep; ++r) {
                 const int t = g * kRowsPerStep + r;
                 if (t >= eg) break;
-                if (ok) gstore16(dp[t] + off, make_uint4(acc[g][r][0], acc[g][r][1], acc[g][r][2], acc[g][r][3]));
+                if (ok) gstore16<NT>(dp[t] + off, make_uint4(acc[g][r][0], acc[g][r][1], acc[g][r][2], acc[g][r][3]));
             }
     }
 }
@@ -311,11 +319,13 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint8_t* p, size_
 
 struct Variant {
     int K, MG, BT;
+    bool nt;
     const char* name;
     void (*fn)(MatArgs);
 };
 
-#define RS_VARIANT(K, MG, BT) {K, MG, BT, "K" #K "_MG" #MG "_B" #BT, rs_matmul_kernel<K, MG, BT>}
+#define RS_VARIANT(K, MG, BT) {K, MG, BT, true, "K" #K "_MG" #MG "_B" #BT, rs_matmul_kernel<K, MG, BT, true>}
+#define RS_VARIANT_T(K, MG, BT) {K, MG, BT, false, "K" #K "_MG" #MG "_B" #BT "_T", rs_matmul_kernel<K, MG, BT, false>}
 // Specialised variants for the configurations the plugin and BASELINE use,
 // then runtime-k fall-backs (k up to 256).
 const Variant kVariants[] = {
@@ -325,16 +335,25 @@ const Variant kVariants[] = {
     RS_VARIANT(64, 16, 256),  // RS(64,16): BASELINE config 5
     RS_VARIANT(0, 4, 256),
     RS_VARIANT(0, 8, 256),
+    // Temporal-policy twin of the headline variant, for A/B (RSMI_NT=0).
+    RS_VARIANT_T(10, 4, 256),
     // 512/1024-thread blocks measured 3-13% slower for RS(10,4) on one box
     // (profiles/r01_ab_block.log); RSMI_BLOCK selects among compiled sizes.
 };
 #undef RS_VARIANT
+#undef RS_VARIANT_T
 
 const Variant& pick(int k, int m) {
     static const int want_bt = [] {
         const char* e = std::getenv("RSMI_BLOCK");  // tuning knob
         return e ? std::atoi(e) : 256;
     }();
+    static const bool want_nt = [] {
+        const char* e = std::getenv("RSMI_NT");  // tuning knob (default 1: non-temporal)
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    for (const Variant& v : kVariants)
+        if (v.K != 0 && v.K == k && m <= v.MG && v.BT == want_bt && v.nt == want_nt) return v;
     for (const Variant& v : kVariants)
         if (v.K != 0 && v.K == k && m <= v.MG && v.BT == want_bt) return v;
     for (const Variant& v : kVariants)
