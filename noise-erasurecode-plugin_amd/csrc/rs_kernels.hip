@@ -198,7 +198,11 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     // their HBM latency; with one iteration per block (the default) this is
     // the whole data path.
     uint4 xpre[kRegPtrs ? K : 1];
-    const uint32_t col0 = chunk * a.iters * BT + threadIdx.x;
+    // Iteration it of block `chunk` codes column chunk (it * chunks + chunk):
+    // blocks running together stay on adjacent 4 KiB pieces of the same
+    // shards (DRAM row locality) whatever the iteration count.
+    const uint32_t cstride = a.chunks * BT;
+    const uint32_t col0 = chunk * BT + threadIdx.x;
     const uint32_t off0 = (col0 <= last ? col0 : last) * 16u;
     if constexpr (kRegPtrs) {
 #pragma unroll
@@ -232,7 +236,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     __syncthreads();
 
     for (uint32_t it = 0; it < a.iters; ++it) {
-        const uint32_t colbase = (chunk * a.iters + it) * BT;
+        const uint32_t colbase = chunk * BT + it * cstride;
         if (colbase >= a.ncols16) break;
         RS_MEM_FENCE();
         const uint32_t col = colbase + threadIdx.x;
@@ -282,8 +286,8 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
         if constexpr (kRegPtrs) {
             // Software pipelining: the next iteration's survivor loads go out
             // before this iteration's stores.
-            const uint32_t ncol = colbase + BT + threadIdx.x;
-            if (it + 1 < a.iters && colbase + BT < a.ncols16) {
+            const uint32_t ncol = colbase + cstride + threadIdx.x;
+            if (it + 1 < a.iters && colbase + cstride < a.ncols16) {
                 const uint32_t noff = (ncol <= last ? ncol : last) * 16u;
 #pragma unroll
                 for (int j = 0; j < K; ++j) xpre[j] = gload16<NT>(sp[j] + noff);
