@@ -69,7 +69,7 @@ def main():
     lines.append("")
     lines.append("Per role (launch order alternates encode / reconstruct):")
     lines.append("")
-    lines.append("| role | launches | avg ms | VGPR | grid |")
+    lines.append("| role | launches | avg ms | grid (threads) | workgroup |")
     lines.append("|---|---|---|---|---|")
     avg = {}
     for role, rs in roles.items():
@@ -77,8 +77,8 @@ def main():
         if not d:
             continue
         avg[role] = statistics.mean(d)
-        lines.append(f"| {role} | {len(d)} | {avg[role]:.3f} | {rs[0].get('VGPR_Count', '?')} | "
-                     f"{rs[0].get('Grid_Size', '?')} |")
+        lines.append(f"| {role} | {len(d)} | {avg[role]:.3f} | {rs[0].get('Grid_Size_X', '?')} | "
+                     f"{rs[0].get('Workgroup_Size_X', '?')} |")
     lines.append("")
 
     traffic = {}
@@ -92,6 +92,9 @@ def main():
     lines.append("FETCH_SIZE x 1024 x 2 (gfx950: FETCH_SIZE counts half of a wide streaming read), "
                  "WRITE_SIZE x 1024 (exact for 16-B stores).")
     lines.append("")
+    lines.append("Reconstruct algorithmic bytes are the expectation k + (m+1)/2 shards per stripe "
+                 "(uniform 1..m erasures); the profiled launches drew their own random sets.")
+    lines.append("")
     lines.append("| role | FETCH_SIZE KiB | read GB (corrected) | WRITE_SIZE KiB | write GB | traffic GB | algorithmic GB | traffic / algorithmic |")
     lines.append("|---|---|---|---|---|---|---|---|")
     for role in roles:
@@ -104,7 +107,8 @@ def main():
         if role == "encode":
             alg = alg_enc
         else:
-            alg = None
+            # bench.py draws 1..m erasures uniformly: E[e] = (m + 1) / 2
+            alg = st * (k + (n - k + 1) / 2) * S
         t = rd + wr
         traffic[f"{role}_k{k}_n{n}_S{S}_stripes{st}"] = round(t / 1e9, 3)
         lines.append(f"| {role} | {statistics.mean(f):.0f} | {rd/1e9:.2f} | {statistics.mean(w):.0f} | "
