@@ -266,10 +266,11 @@ def main():
                 "reconstruct_ms": round(rec_avg_ms, 3),
                 "reconstruct_GBps": round(rec_avg_bytes / (rec_avg_ms / 1e3) / 1e9, 1) if do_rec else None,
                 "reconstruct_frac": round(rec_avg_bytes / (rec_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if do_rec else None,
-                "kernel_variant": rsmi_variant(k, n),
+                "encode_kernel": f.kernel_name(0),
+                "reconstruct_kernel": f.kernel_name(1),
             },
             "roofline": {
-                "kernel": f"rs_matmul_kernel ({dominant})",
+                "kernel": f"{f.kernel_name(0 if do_enc else 1)} ({dominant})",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -366,15 +367,6 @@ def sharded_main(args, world, rank, local, dev, distributed):
         }), flush=True)
     if distributed:
         torch.distributed.destroy_process_group()
-
-
-def rsmi_variant(k, n):
-    m = n - k
-    if k == 10 and m <= 4:
-        return "K10_MG4"
-    if k == 64 and m <= 16:
-        return "K64_MG16"
-    return "generic"
 
 
 if __name__ == "__main__":

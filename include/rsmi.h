@@ -64,6 +64,10 @@ int rs_device(const rs_ctx *ctx);
 /* Copy of the n x k row-major encode matrix (infectious FEC.enc_matrix). */
 int rs_encode_matrix(const rs_ctx *ctx, uint8_t *out);
 const char *rs_strerror(int status);
+/* Diagnostics: name of the kernel that serves encode (which = 0) or
+ * reconstruct (which = 1) for this ctx, e.g. "bitslice_k64_m16" or
+ * "K10_MG4_B256" (no reference counterpart). */
+const char *rs_kernel_name(const rs_ctx *ctx, int which);
 
 /* ---- host-buffer API (the cgo path) -------------------------------------
  * rs_encode replaces (*FEC).Encode(input, output) at main.go:262.

@@ -16,6 +16,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "bitslice.hpp"
 #include "gf256.hpp"
 #include "gf_invert.hpp"
 #include "host_pipeline.hpp"
@@ -126,6 +127,9 @@ struct Staging {
 struct rs_ctx {
     int k = 0, n = 0, m = 0, device = 0;
     std::vector<uint8_t> enc;  // n x k systematic matrix
+    // Generated bit-sliced encode kernel for this (k, n), if one was built
+    // and its embedded matrix equals enc (bitslice.hpp); nullptr otherwise.
+    const rsmi::BitsliceKernel* bitslice = nullptr;
     std::mutex mu;
     hipStream_t stream = nullptr;  // used by the host-buffer API
 
@@ -233,6 +237,36 @@ rsmi::MatArgs base_args(rs_ctx* c, void* data, size_t dss, void* parity, size_t 
     a.k = static_cast<uint32_t>(c->k);
     a.m = static_cast<uint32_t>(c->m);
     return a;
+}
+
+// Generated bit-sliced encode kernel for (k, m) if the build has one whose
+// embedded matrix is this context's.  By default it serves the codes whose
+// split-table encode is VALU-bound (k*m >= 256, e.g. RS(64,16)); the
+// RSMI_BITSLICE knob forces it on (1) or off (0) for A/B runs.
+const rsmi::BitsliceKernel* pick_bitslice(const std::vector<uint8_t>& enc, int k, int m) {
+    const char* e = std::getenv("RSMI_BITSLICE");
+    if (e && std::atoi(e) == 0) return nullptr;
+    if (!e && k * m < 256) return nullptr;
+    const rsmi::BitsliceKernel* b = rsmi::bitslice_kernel(k, m);
+    if (!b) return nullptr;
+    const uint8_t* bottom = enc.data() + static_cast<size_t>(k) * k;
+    return std::memcmp(b->matrix, bottom, static_cast<size_t>(m) * k) == 0 ? b : nullptr;
+}
+
+// Encode launch (all parity rows of every stripe): the generated bit-sliced
+// kernel when there is one for this code, else the split-table kernel.
+hipError_t launch_encode(rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s) {
+    if (!c->bitslice) return rsmi::launch_matmul(a, c->m, s);
+    rsmi::BitsliceArgs b{};
+    b.data = a.data;
+    b.parity = a.parity;
+    b.data_ss = a.data_ss;
+    b.parity_ss = a.parity_ss;
+    b.pitch = a.pitch;
+    b.stripes = a.stripes;
+    b.ncols16 = a.ncols16;
+    b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
+    return c->bitslice->launch(b, s);
 }
 
 // Finds or creates the decode pattern for `erased` (n flags); -1 on error
@@ -535,6 +569,7 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     c->m = n - k;
     c->device = device;
     c->enc = rsmi::systematic_matrix(k, n);
+    c->bitslice = pick_bitslice(c->enc, k, c->m);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RS_EDEVICE;
@@ -601,6 +636,12 @@ int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
     if (!c || !out) return RS_EINVAL;
     std::memcpy(out, c->enc.data(), c->enc.size());
     return RS_OK;
+}
+
+const char* rs_kernel_name(const rs_ctx* c, int which) {
+    if (!c) return "";
+    if (which == 0 && c->bitslice) return c->bitslice->name;
+    return rsmi::variant_name(c->k, c->m);
 }
 
 int rs_pattern_count(const rs_ctx* c) {
@@ -675,7 +716,7 @@ int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, siz
     rsmi::MatArgs a = base_args(c, const_cast<void*>(data), dss, parity, pss, pitch, len, stripes);
     set_patterns(c, 1, c->d_encpat.p, a);
     a.stripe_desc = nullptr;
-    return hip_status(rsmi::launch_matmul(a, c->m, static_cast<hipStream_t>(stream)));
+    return hip_status(launch_encode(c, a, static_cast<hipStream_t>(stream)));
 }
 
 int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
@@ -758,7 +799,7 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     auto launch = [c](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
         rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
         set_patterns(c, 1, c->d_encpat.p, a);
-        return rsmi::launch_matmul(a, c->m, st);
+        return launch_encode(c, a, st);
     };
     return hip_status(c->pipe->run(srcs.data(), c->k, dsts.data(), c->m, S, launch));
 }

@@ -38,7 +38,7 @@ EXPORTS = (
     "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_prepare_patterns",
     "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
-    "rs_stream_sync", "rs_fill_splitmix",
+    "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
 )
 
 
@@ -77,6 +77,7 @@ def _lib() -> ctypes.CDLL:
             "rs_device": (i32, [vp]),
             "rs_encode_matrix": (i32, [vp, u8p]),
             "rs_strerror": (ctypes.c_char_p, [i32]),
+            "rs_kernel_name": (ctypes.c_char_p, [vp, i32]),
             "rs_encode": (i32, [vp, vp, sz, vp]),
             "rs_decode": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(vp), i32, sz, vp]),
             "rs_decode_batch": (i32, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32),
@@ -161,6 +162,10 @@ class FEC:
             self.close()
         except Exception:
             pass
+
+    def kernel_name(self, which: int = 0) -> str:
+        """Kernel serving encode (0) or reconstruct (1): diagnostics."""
+        return _lib().rs_kernel_name(self._h, which).decode()
 
     def matrix(self) -> bytes:
         buf = (ctypes.c_uint8 * (self.n * self.k))()
