@@ -11,6 +11,15 @@
 // XORs building the 4-plane combinations (method of four Russians), then one
 // v_bitop3 (3-way XOR) per output plane -- about 5 VALU ops per byte of
 // traffic instead of 17.
+//
+// Reconstruct (k <= 64) reuses the fixed network through syndromes: with the
+// erased data shards read as zero, the network yields q_t = sum over present
+// data of E[t][j] * d_j for every parity row t.  For each parity survivor t,
+// s_t = p_t ^ q_t depends on the erased data alone, and every output is
+//     out_o = sum_t row_o[slot(t)] * s_t  (^ q_o if output o is parity o),
+// where row_o is the pattern's decode row (gf_invert.hip) and slot(t) the
+// survivor slot Rebuild gave parity t.  The per-pattern part is an e x d
+// split-table product on d <= m syndromes instead of e x k on the survivors.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,11 +39,31 @@ struct BitsliceArgs {
 
 using BitsliceLaunch = hipError_t (*)(const BitsliceArgs&, hipStream_t);
 
+// Reconstruct launch: same stripe descriptors and pattern cache as the
+// split-table kernel (rs_kernels.hpp MatArgs).
+struct BitsliceRecArgs {
+    uint8_t* data;               // shard id i < k at data + s*data_ss + i*pitch
+    uint8_t* parity;             // shard id k + t at parity + s*parity_ss + t*pitch
+    uint64_t data_ss, parity_ss, pitch;
+    uint64_t count;              // descriptors
+    const uint2* stripe_desc;    // [count] {stripe, pattern id << 8 | outputs}
+    const uint8_t* coef;         // [npat][m][k] decode rows
+    const uint32_t* src;         // [npat][k] survivor ids (Rebuild's slots)
+    const uint32_t* dst;         // [npat][dst_stride] output ids
+    uint32_t dst_stride;
+    uint32_t ncols16;
+    uint32_t blocks_per_stripe;
+};
+
+using BitsliceRecLaunch = hipError_t (*)(const BitsliceRecArgs&, hipStream_t);
+
 struct BitsliceKernel {
     int k, m;
     const char* name;       // "bitslice_k<k>_m<m>"
     const uint8_t* matrix;  // [m][k] parity rows the kernel was generated from
     BitsliceLaunch launch;
+    const char* rec_name;         // "bitslice_rec_k<k>_m<m>", or nullptr
+    BitsliceRecLaunch reconstruct;  // nullptr when k > 64
 };
 
 // Generated kernel for encode of (k, k+m), or nullptr.

@@ -4,10 +4,8 @@
 // (*FEC).Rebuild (reference call site main.go:77), batched over stripes.
 //
 // Arithmetic (no MFMA: GF(2^8) is not an FP contraction):
-//   c * x for a byte x is split over the bit fields x[2:0], x[5:3], x[7:6]:
-//       c*x = Ta[x & 7] ^ Tb[(x >> 3) & 7] ^ Tc[x >> 6]
-//   Ta/Tb are 8-entry byte tables (two dwords each), Tc a 4-entry table (one
-//   dword); each lookup is one v_perm_b32 on four packed bytes at once.
+//   split-table GF(2^8) multiply (gf_device.hpp): three v_perm_b32 lookups
+//   per coefficient on four packed bytes at once.
 //   The five table dwords per coefficient are built per block from the raw
 //   coefficient bytes and staged in LDS; a lane reads a coefficient's tables
 //   with broadcast ds_read_b128 and XOR-accumulates in VGPRs (v_bitop3_b32).
@@ -15,6 +13,8 @@
 // (global_load_dwordx4, fully coalesced: 64 lanes = 1 KiB contiguous per
 // shard); outputs are written once with global_store_dwordx4.
 #include "rs_kernels.hpp"
+
+#include "gf_device.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -24,47 +24,9 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-__device__ __forceinline__ uint32_t xtime(uint32_t a) {
-    a <<= 1;
-    return a ^ ((a & 0x100u) ? 0x11Du : 0u);
-}
-
-// Split-table words of coefficient c (host twin: gf256.cpp coef_tables).
-__device__ void build_tables(uint32_t c, uint32_t* w) {
-    uint32_t p[8];
-    p[0] = c;
-#pragma unroll
-    for (int b = 1; b < 8; ++b) p[b] = xtime(p[b - 1]);
-    auto val = [&](uint32_t v) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) r ^= ((v >> b) & 1u) ? p[b] : 0u;
-        return r;
-    };
-    auto pack = [&](uint32_t base, uint32_t step) {
-        return val(base) | (val(base + step) << 8) | (val(base + 2 * step) << 16) |
-               (val(base + 3 * step) << 24);
-    };
-    w[0] = pack(0, 1);
-    w[1] = pack(4, 1);
-    w[2] = pack(0, 8);
-    w[3] = pack(32, 8);
-    w[4] = pack(0, 64) & 0xFFFFFFFFu;
-}
-
-// acc ^= c * x on four packed bytes, c given by its table words T[0..4];
-// ia/ib/ic are the per-byte bit-field selectors of x.
-__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, const uint32_t* T, uint32_t ia,
-                                           uint32_t ib, uint32_t ic) {
-    const uint32_t la = __builtin_amdgcn_perm(T[1], T[0], ia);
-    const uint32_t lb = __builtin_amdgcn_perm(T[3], T[2], ib);
-    const uint32_t lc = __builtin_amdgcn_perm(T[4], T[4], ic);
-    return xor3(acc, la, lb) ^ lc;
-}
+using gfd::build_tables;
+using gfd::gf_mac;
+using gfd::xor3;
 
 // Compiler fence for memory operations: keeps LDS table reads where they are
 // written (LICM would otherwise hoist all k*MG*5 table dwords into VGPRs).

@@ -130,6 +130,9 @@ struct rs_ctx {
     // Generated bit-sliced encode kernel for this (k, n), if one was built
     // and its embedded matrix equals enc (bitslice.hpp); nullptr otherwise.
     const rsmi::BitsliceKernel* bitslice = nullptr;
+    bool bitslice_rec = false;  // batched reconstruct uses bitslice->reconstruct ...
+    int bitslice_rec_min_e = 1;  // ... for stripes with at least this many erasures
+    std::string rec_name;        // rs_kernel_name(ctx, 1) when bitslice_rec
     std::mutex mu;
     hipStream_t stream = nullptr;  // used by the host-buffer API
 
@@ -267,6 +270,18 @@ hipError_t launch_encode(rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s) {
     b.ncols16 = a.ncols16;
     b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
     return c->bitslice->launch(b, s);
+}
+
+// Batched reconstruct through the generated bit-sliced kernel: whenever the
+// code's encode is bit-sliced and a reconstruct twin was generated (k <= 64).
+// RSMI_BITSLICE_REC=0 keeps the split-table kernel (A/B runs).
+// Read at rs_new, like RSMI_BITSLICE.
+bool use_bitslice_rec(const rs_ctx* c) { return c->bitslice_rec; }
+
+bool pick_bitslice_rec(const rsmi::BitsliceKernel* b) {
+    const char* e = std::getenv("RSMI_BITSLICE_REC");
+    if (e && std::atoi(e) == 0) return false;
+    return b && b->reconstruct;
 }
 
 // Finds or creates the decode pattern for `erased` (n flags); -1 on error
@@ -570,6 +585,17 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     c->device = device;
     c->enc = rsmi::systematic_matrix(k, n);
     c->bitslice = pick_bitslice(c->enc, k, c->m);
+    c->bitslice_rec = pick_bitslice_rec(c->bitslice);
+    {
+        // RS(64,16): the split-table kernel wins up to one 4-row group (e <= 4).
+        const char* ev = std::getenv("RSMI_BITSLICE_REC_MIN_E");
+        c->bitslice_rec_min_e = ev ? std::max(1, std::atoi(ev)) : 5;
+        if (c->bitslice_rec)
+            c->rec_name = c->bitslice_rec_min_e <= 1
+                              ? std::string(c->bitslice->rec_name)
+                              : std::string(rsmi::variant_name(k, c->m)) + " (e<" +
+                                    std::to_string(c->bitslice_rec_min_e) + ") + " + c->bitslice->rec_name;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RS_EDEVICE;
@@ -641,6 +667,7 @@ int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
 const char* rs_kernel_name(const rs_ctx* c, int which) {
     if (!c) return "";
     if (which == 0 && c->bitslice) return c->bitslice->name;
+    if (which == 1 && use_bitslice_rec(c)) return c->rec_name.c_str();
     return rsmi::variant_name(c->k, c->m);
 }
 
@@ -750,17 +777,30 @@ static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, s
         max_e = std::max<int>(max_e, static_cast<int>(c->h_cnt[id]));
     }
     if (max_e == 0) return RS_OK;  // nothing erased anywhere
-    // Counting sort of the stripes by pattern (bucket = pattern id; the
-    // RSMI_NO_SORT knob keeps address order for A/B runs).
+    // Split between the kernels: with a bit-sliced reconstruct, stripes with
+    // few outputs still go to the split-table kernel, whose cost grows with
+    // e while the syndrome network costs a whole encode (RS(64,16), one box:
+    // e=4 15.9 vs 18.6 ms, e=8 23.1 vs 20.0 ms; profiles/r01_ab_bitslice_rec.log).
+    const int split_e = use_bitslice_rec(c) ? c->bitslice_rec_min_e : (c->m + 1);
+    auto high = [&](uint32_t p) { return static_cast<int>(c->h_cnt[p]) >= split_e; };
+    // Counting sort of the stripes by (kernel, pattern): each launch lists its
+    // stripes grouped by pattern (see rs_kernels.hpp stripe_desc).  The
+    // RSMI_NO_SORT knob keeps address order within a kernel (A/B runs).
     static const bool no_sort = std::getenv("RSMI_NO_SORT") != nullptr;
-    const size_t nb = no_sort ? 1 : c->h_cnt.size();
-    auto bucket = [&](size_t i) -> size_t { return no_sort ? 0 : pid[i]; };
+    const size_t npat = no_sort ? 1 : c->h_cnt.size();
+    const size_t nb = 2 * npat;
+    auto bucket = [&](size_t i) -> size_t { return (high(pid[i]) ? npat : 0) + (no_sort ? 0 : pid[i]); };
     std::vector<uint32_t>& start = c->scratch_start;
     start.assign(nb + 1, 0);
-    for (size_t i = 0; i < stripes; ++i)
-        if (c->h_cnt[pid[i]]) ++start[bucket(i) + 1];  // stripes with nothing erased are skipped
+    int max_lo = 0;
+    for (size_t i = 0; i < stripes; ++i) {
+        const uint32_t p = pid[i];
+        if (!c->h_cnt[p]) continue;  // stripes with nothing erased are skipped
+        ++start[bucket(i) + 1];
+        if (!high(p)) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
+    }
     for (size_t b = 0; b < nb; ++b) start[b + 1] += start[b];
-    const size_t used = start[nb];
+    const size_t used = start[nb], n_lo = start[npat];
     if (!c->st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
     uint2* desc = static_cast<uint2*>(c->st_stripe.p);
     for (size_t i = 0; i < stripes; ++i) {
@@ -774,10 +814,36 @@ static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, s
                                   hipMemcpyHostToDevice, s);
     c->st_stripe.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
-    rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used);
-    set_cache_patterns(c, a);
-    a.stripe_desc = static_cast<const uint2*>(c->d_stripe_pat.p);
-    return hip_status(rsmi::launch_matmul(a, max_e, s));
+    const uint2* d_desc = static_cast<const uint2*>(c->d_stripe_pat.p);
+    if (n_lo > 0) {
+        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, n_lo);
+        set_cache_patterns(c, a);
+        a.stripe_desc = d_desc;
+        e = rsmi::launch_matmul(a, max_lo, s);
+        if (e != hipSuccess) return RS_EDEVICE;
+    }
+    if (used > n_lo) {
+        // Generated bit-sliced reconstruct (syndromes through the fixed
+        // encode network, bitslice.hpp): same descriptors and pattern cache.
+        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used - n_lo);
+        set_cache_patterns(c, a);
+        rsmi::BitsliceRecArgs b{};
+        b.data = a.data;
+        b.parity = a.parity;
+        b.data_ss = a.data_ss;
+        b.parity_ss = a.parity_ss;
+        b.pitch = a.pitch;
+        b.count = a.stripes;
+        b.stripe_desc = d_desc + n_lo;
+        b.coef = a.coef;
+        b.src = a.src;
+        b.dst = a.dst;
+        b.dst_stride = a.dst_stride;
+        b.ncols16 = a.ncols16;
+        b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
+        e = c->bitslice->reconstruct(b, s);
+    }
+    return hip_status(e);
 }
 extern "C" {
 

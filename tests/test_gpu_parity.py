@@ -229,6 +229,128 @@ def test_bitslice_host_api_encode_matches_table_kernel():
     b.close()
 
 
+def _fec_env(k, n, **env):
+    """FEC built with RSMI_* knobs set (the kernel choice is made at rs_new)."""
+    old = {key: os.environ.get(key) for key in env}
+    os.environ.update(env)
+    try:
+        return rsmi.NewFEC(k, n)
+    finally:
+        for key, v in old.items():
+            if v is None:
+                del os.environ[key]
+            else:
+                os.environ[key] = v
+
+
+def test_bitslice_reconstruct_kernel_selection():
+    """Batched reconstruct of a bit-sliced code goes through the generated
+    syndrome kernel (bitslice.hpp) unless RSMI_BITSLICE_REC=0."""
+    assert fec(64, 80).kernel_name(1) == "K64_MG16_B256 (e<5) + bitslice_rec_k64_m16"
+    assert _fec_env(64, 80, RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == "bitslice_rec_k64_m16"
+    assert _fec_env(64, 80, RSMI_BITSLICE_REC="0").kernel_name(1).startswith("K64_MG16")
+    assert fec(10, 14).kernel_name(1).startswith("K10_MG4")
+    assert _fec_env(10, 14, RSMI_BITSLICE="1", RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == \
+        "bitslice_rec_k10_m4"
+
+
+def _fixed_patterns(k, n):
+    """Edge erasure sets: every single erasure, all-data, all-parity, the
+    m highest data shards, alternating, and the first/last shard pairs."""
+    m = n - k
+    pats = [[i] for i in range(n)]
+    pats += [list(range(min(m, k))), list(range(k, n)), list(range(k - min(m, k), k)),
+             list(range(0, n, 2))[:m], [0, n - 1], [k - 1, k]]
+    out = np.zeros((len(pats), n), dtype=np.uint8)
+    for r, p in enumerate(pats):
+        out[r, p[:m]] = 1
+    return out
+
+
+@pytest.mark.parametrize("k,n", [(64, 80), (10, 14)])
+@pytest.mark.parametrize("S,pitch", [(16, 16), (17, 32), (1000, 1008), (8192 + 16, 8208),
+                                     (65536, 65536), (100000, 100000)])
+def test_bitslice_reconstruct_roundtrip(k, n, S, pitch):
+    """Generated bit-sliced reconstruct: random 1..m erasures plus the edge
+    patterns, ragged shard lengths; regenerated shards equal the originals
+    and the split-table kernel's output (both must be the unique codeword)."""
+    m = n - k
+    fb = _fec_env(k, n, RSMI_BITSLICE="1", RSMI_BITSLICE_REC_MIN_E="1")  # every stripe
+    ft = _fec_env(k, n, RSMI_BITSLICE="0", RSMI_BITSLICE_REC="0")
+    assert fb.kernel_name(1).startswith("bitslice_rec") and "bitslice" not in ft.kernel_name(1)
+    rng = np.random.default_rng(k * 7 + S)
+    er = np.concatenate([_fixed_patterns(k, n), _erasures(rng, 24, n, m)])
+    stripes = len(er)
+    data, parity = _dev_stripes(fb, stripes, S, pitch, 17 + S)
+    fb.encode_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes)
+    fb.sync()
+    d0, p0 = data.clone(), parity.clone()
+    for f in (fb, ft):
+        data.copy_(d0)
+        parity.copy_(p0)
+        dv, pv = data.view(stripes, k, pitch), parity.view(stripes, m, pitch)
+        dv[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0xA5
+        pv[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0x5A
+        f.reconstruct_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S,
+                              stripes, er.tobytes())
+        f.sync()
+        dv0, pv0 = d0.view(stripes, k, pitch), p0.view(stripes, m, pitch)
+        assert torch.equal(dv[:, :, :S], dv0[:, :, :S]), f.kernel_name(1)
+        assert torch.equal(pv[:, :, :S], pv0[:, :, :S]), f.kernel_name(1)
+    fb.close()
+    ft.close()
+
+
+def test_reconstruct_split_between_kernels():
+    """Default RS(64,16) reconstruct: stripes with e < 5 go to the split-table
+    kernel, the rest to the syndrome kernel, in one call (two launches)."""
+    k, n, S = 64, 80, 8192
+    m = n - k
+    f = fec(64, 80)
+    rng = np.random.default_rng(77)
+    er = np.concatenate([_erasures(rng, 10, n, m, emin=1, emax=4),
+                         _erasures(rng, 10, n, m, emin=5, emax=16)])
+    er = er[rng.permutation(len(er))]
+    stripes = len(er)
+    data, parity = _dev_stripes(f, stripes, S, S, 91)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    d0, p0 = data.clone(), parity.clone()
+    data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+    parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                          er.tobytes())
+    f.sync()
+    assert torch.equal(data, d0) and torch.equal(parity, p0)
+
+
+def test_bitslice_reconstruct_matches_oracle_rebuild():
+    """RS(64,16) through the syndrome kernel: the regenerated data shards are
+    the oracle's Rebuild of the same survivors (byte for byte)."""
+    k, n, S, stripes = 64, 80, 4096, 6
+    m = n - k
+    f = fec(64, 80)
+    data, parity = _dev_stripes(f, stripes, S, S, 2024)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    er = _erasures(np.random.default_rng(5), stripes, n, m, emin=m - 2, emax=m)
+    hd = data.cpu().numpy().reshape(stripes, k, S).copy()
+    hp = parity.cpu().numpy().reshape(stripes, m, S).copy()
+    E = oracle.fec_matrix(k, n)
+    data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+    parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                          er.tobytes())
+    f.sync()
+    got = data.cpu().numpy().reshape(stripes, k, S)
+    for s in range(stripes):
+        sh = [hd[s, i].tobytes() for i in range(k)] + [hp[s, i].tobytes() for i in range(m)]
+        keep = [i for i in range(n) if not er[s, i]]
+        rc, ref = oracle.decode(E, k, n, [(i, sh[i]) for i in keep[:k]])
+        assert rc == 0 and ref == got[s].tobytes(), s
+    assert parity.cpu().numpy().reshape(stripes, m, S).tobytes() == hp.tobytes()
+
+
 def test_fill_splitmix_matches_oracle():
     f = fec(10, 14)
     for n_bytes in (1, 7, 8, 4099, 1 << 16):

@@ -30,6 +30,52 @@ def matmul_only(rs):
     return [r for r in rs if "rs_matmul_kernel" in r["Kernel_Name"]]
 
 
+def coding_kernels(rs):
+    """Launches of the engine's coding kernels (split-table and bit-sliced)."""
+    return [r for r in rs if "rs_matmul_kernel" in r["Kernel_Name"] or "rs_bitslice" in r["Kernel_Name"]]
+
+
+def short_name(name):
+    for key in ("rs_bitslice_rec_k", "rs_bitslice_k"):
+        if key in name:
+            return name[name.index(key):].split("(")[0].split("E")[0]
+    if "rs_matmul_kernel<" in name:
+        return name[name.index("rs_matmul_kernel<"):].split(">")[0] + ">"
+    return name[:60]
+
+
+def by_name_section(a):
+    """Per coding kernel: launches, average duration, HBM bytes per launch."""
+    tr = coding_kernels(rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv")))
+    if not tr:
+        return []
+    out = ["## Per coding kernel (trace + separate FETCH_SIZE / WRITE_SIZE passes)", "",
+           "| kernel | launches | avg ms | read GB/launch (FETCH x2) | write GB/launch | traffic GB/launch | HBM GB/s |",
+           "|---|---|---|---|---|---|---|"]
+    pmc = {}
+    for cnt, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        for r in coding_kernels(rows(os.path.join(a.dir, sub, "run_counter_collection.csv"))):
+            if r["Counter_Name"] == cnt:
+                pmc.setdefault((short_name(r["Kernel_Name"]), cnt), []).append(float(r["Counter_Value"]))
+    names = []
+    for r in tr:
+        nm = short_name(r["Kernel_Name"])
+        if nm not in names:
+            names.append(nm)
+    for nm in names:
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr
+             if short_name(r["Kernel_Name"]) == nm]
+        f = pmc.get((nm, "FETCH_SIZE"), [])
+        w = pmc.get((nm, "WRITE_SIZE"), [])
+        rd = statistics.mean(f) * 1024 * 2 / 1e9 if f else float("nan")
+        wr = statistics.mean(w) * 1024 / 1e9 if w else float("nan")
+        ms = statistics.mean(d)
+        out.append(f"| `{nm}` | {len(d)} | {ms:.3f} | {rd:.2f} | {wr:.2f} | {rd + wr:.2f} | "
+                   f"{(rd + wr) / (ms / 1e3):.0f} |")
+    out.append("")
+    return out
+
+
 def split_roles(rs, mode):
     """bench --mode both: launches alternate encode, reconstruct."""
     if mode == "both":
@@ -119,6 +165,7 @@ def main():
         ach = alg_enc / (avg["encode"] / 1e3) / 1e9
         lines.append(f"Encode: algorithmic {alg_enc/1e9:.2f} GB per launch / {avg['encode']:.3f} ms = "
                      f"**{ach:.0f} GB/s = {ach/8000:.1%} of 8 TB/s**.")
+    lines += by_name_section(a)
     if a.bench_log and os.path.exists(a.bench_log):
         for line in open(a.bench_log):
             if line.startswith("{"):
