@@ -44,6 +44,20 @@ def short_name(name):
     return name[:60]
 
 
+def kernel_traffic_gb(a, key):
+    """Mean FETCH_SIZE x2 + WRITE_SIZE (GB) per launch of kernels whose name
+    contains key (and not "_rec" unless asked), or None."""
+    vals = {}
+    for cnt, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        v = [float(r["Counter_Value"]) for r in rows(os.path.join(a.dir, sub, "run_counter_collection.csv"))
+             if r["Counter_Name"] == cnt and key in r["Kernel_Name"]
+             and ("_rec" in key or "_rec" not in r["Kernel_Name"])]
+        if not v:
+            return None
+        vals[cnt] = statistics.mean(v)
+    return (vals["FETCH_SIZE"] * 2 + vals["WRITE_SIZE"]) * 1024 / 1e9
+
+
 def by_name_section(a):
     """Per coding kernel: launches, average duration, HBM bytes per launch."""
     tr = coding_kernels(rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv")))
@@ -99,8 +113,12 @@ def main():
     m = n - k
     alg_enc = st * (k + m) * S
 
-    tr = matmul_only(rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv")))
-    roles = split_roles(tr, a.mode)
+    all_tr = rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv"))
+    # With generated bit-sliced kernels in the run, encode and reconstruct are
+    # told apart by kernel name (per-kernel section below), not launch order.
+    has_bs = any("rs_bitslice" in r["Kernel_Name"] for r in all_tr)
+    tr = matmul_only(all_tr)
+    roles = {} if has_bs else split_roles(tr, a.mode)
     lines = [f"# rocprofv3 summary: {os.path.basename(os.path.normpath(a.dir))}", ""]
     lines.append(f"Workload: RS({k},{n}), {st} stripes x {k} x {S} B shards, bench.py --mode {a.mode}.")
     lines.append("")
@@ -113,19 +131,37 @@ def main():
         lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
                      f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} | {float(r['Percentage']):.2f} |")
     lines.append("")
-    lines.append("Per role (launch order alternates encode / reconstruct):")
-    lines.append("")
-    lines.append("| role | launches | avg ms | grid (threads) | workgroup |")
-    lines.append("|---|---|---|---|---|")
+    bs_traffic = {}
+    if has_bs:
+        lines += by_name_section(a)
+        enc = [r for r in all_tr if "rs_bitslice_k" in r["Kernel_Name"]]
+        enc_traffic = kernel_traffic_gb(a, "rs_bitslice_k")
+        if enc_traffic is not None:
+            bs_traffic[f"encode_k{k}_n{n}_S{S}_stripes{st}"] = round(enc_traffic, 3)
+        if enc:
+            ms = statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in enc)
+            ach = alg_enc / (ms / 1e3) / 1e9
+            lines.append(f"Encode (`{short_name(enc[0]['Kernel_Name'])}`): algorithmic {alg_enc/1e9:.2f} GB per "
+                         f"launch / {ms:.3f} ms = **{ach:.0f} GB/s = {ach/8000:.1%} of 8 TB/s**.")
+        rec = [r for r in all_tr if "rs_bitslice_rec" in r["Kernel_Name"]]
+        if rec:
+            lines.append("")
+            lines.append(f"Reconstruct per step = the split-table launch (stripes with e < 5) plus the "
+                         f"syndrome launch; expected algorithmic bytes {st * (k + (m + 1) / 2) * S / 1e9:.2f} GB "
+                         f"(uniform 1..m erasures).")
+    rl = ["Per role (launch order alternates encode / reconstruct):"]
+    rl.append("")
+    rl.append("| role | launches | avg ms | grid (threads) | workgroup |")
+    rl.append("|---|---|---|---|---|")
     avg = {}
     for role, rs in roles.items():
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rs]
         if not d:
             continue
         avg[role] = statistics.mean(d)
-        lines.append(f"| {role} | {len(d)} | {avg[role]:.3f} | {rs[0].get('Grid_Size_X', '?')} | "
+        rl.append(f"| {role} | {len(d)} | {avg[role]:.3f} | {rs[0].get('Grid_Size_X', '?')} | "
                      f"{rs[0].get('Workgroup_Size_X', '?')} |")
-    lines.append("")
+    rl.append("")
 
     traffic = {}
     pmc = {}
@@ -133,16 +169,16 @@ def main():
         rs = [r for r in matmul_only(rows(os.path.join(a.dir, sub, "run_counter_collection.csv")))
               if r["Counter_Name"] == cnt]
         pmc[cnt] = split_roles(rs, a.mode)
-    lines.append("## HBM traffic (separate --pmc passes, per launch)")
-    lines.append("")
-    lines.append("FETCH_SIZE x 1024 x 2 (gfx950: FETCH_SIZE counts half of a wide streaming read), "
+    rl.append("## HBM traffic (separate --pmc passes, per launch)")
+    rl.append("")
+    rl.append("FETCH_SIZE x 1024 x 2 (gfx950: FETCH_SIZE counts half of a wide streaming read), "
                  "WRITE_SIZE x 1024 (exact for 16-B stores).")
-    lines.append("")
-    lines.append("Reconstruct algorithmic bytes are the expectation k + (m+1)/2 shards per stripe "
+    rl.append("")
+    rl.append("Reconstruct algorithmic bytes are the expectation k + (m+1)/2 shards per stripe "
                  "(uniform 1..m erasures); the profiled launches drew their own random sets.")
-    lines.append("")
-    lines.append("| role | FETCH_SIZE KiB | read GB (corrected) | WRITE_SIZE KiB | write GB | traffic GB | algorithmic GB | traffic / algorithmic |")
-    lines.append("|---|---|---|---|---|---|---|---|")
+    rl.append("")
+    rl.append("| role | FETCH_SIZE KiB | read GB (corrected) | WRITE_SIZE KiB | write GB | traffic GB | algorithmic GB | traffic / algorithmic |")
+    rl.append("|---|---|---|---|---|---|---|---|")
     for role in roles:
         f = [float(r["Counter_Value"]) for r in pmc["FETCH_SIZE"].get(role, [])]
         w = [float(r["Counter_Value"]) for r in pmc["WRITE_SIZE"].get(role, [])]
@@ -157,15 +193,18 @@ def main():
             alg = st * (k + (n - k + 1) / 2) * S
         t = rd + wr
         traffic[f"{role}_k{k}_n{n}_S{S}_stripes{st}"] = round(t / 1e9, 3)
-        lines.append(f"| {role} | {statistics.mean(f):.0f} | {rd/1e9:.2f} | {statistics.mean(w):.0f} | "
+        rl.append(f"| {role} | {statistics.mean(f):.0f} | {rd/1e9:.2f} | {statistics.mean(w):.0f} | "
                      f"{wr/1e9:.2f} | {t/1e9:.2f} | {alg/1e9 if alg else float('nan'):.2f} | "
                      f"{(t/alg) if alg else float('nan'):.3f} |")
-    lines.append("")
+    rl.append("")
+    if not has_bs:
+        lines += rl
     if "encode" in avg:
         ach = alg_enc / (avg["encode"] / 1e3) / 1e9
         lines.append(f"Encode: algorithmic {alg_enc/1e9:.2f} GB per launch / {avg['encode']:.3f} ms = "
                      f"**{ach:.0f} GB/s = {ach/8000:.1%} of 8 TB/s**.")
-    lines += by_name_section(a)
+    if not has_bs:
+        lines += by_name_section(a)
     if a.bench_log and os.path.exists(a.bench_log):
         for line in open(a.bench_log):
             if line.startswith("{"):
@@ -176,6 +215,7 @@ def main():
                              f"{b['breakdown']['reconstruct_ms']} ms.")
     with open(a.out, "w") as fh:
         fh.write("\n".join(lines) + "\n")
+    traffic.update(bs_traffic)
     if a.traffic_json:
         old = {}
         if os.path.exists(a.traffic_json):
