@@ -15,7 +15,8 @@ from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librsmi.so")
+# RSMI_LIB points at another build of the engine (same-box A/B runs of build variants).
+LIB_PATH = os.environ.get("RSMI_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librsmi.so")
 
 # rs_status codes (include/rsmi.h)
 RS_OK = 0
