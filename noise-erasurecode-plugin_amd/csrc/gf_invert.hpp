@@ -20,6 +20,7 @@ struct InvertArgs {
     uint32_t first;          // first pattern id to build
     uint32_t k, m;
     uint32_t* status;        // bit 0 set if a survivor matrix was singular
+    uint32_t generic;        // 1: whole k x k Gauss-Jordan even for Rebuild-shaped survivor sets (A/B)
 };
 
 // Builds patterns [first, first + count): one workgroup each.

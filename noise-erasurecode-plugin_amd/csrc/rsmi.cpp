@@ -369,6 +369,10 @@ int flush_patterns(rs_ctx* c, hipStream_t s) {
     ia.k = static_cast<uint32_t>(c->k);
     ia.m = static_cast<uint32_t>(c->m);
     ia.status = dev_status(c);
+    {
+        const char* g = std::getenv("RSMI_INVERT_GENERIC");
+        ia.generic = g && std::atoi(g) != 0 ? 1u : 0u;
+    }
     e = rsmi::launch_invert(ia, static_cast<uint32_t>(cnt), s);
     if (e != hipSuccess) return RS_EDEVICE;
     c->uploaded = npat;

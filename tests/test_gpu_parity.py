@@ -494,7 +494,7 @@ def _host_rows(k, n, erased):
     return np_rs.matmul(E[tg], inv) if tg else np.zeros((0, k), np.uint8)
 
 
-@pytest.mark.parametrize("k,n,count", [(10, 14, 0), (64, 80, 40), (17, 49, 30), (200, 256, 3),
+@pytest.mark.parametrize("k,n,count", [(10, 14, 0), (64, 80, 40), (17, 49, 30), (200, 256, 3), (100, 228, 4),
                                        (4, 6, 0)])
 def test_gpu_inversion_matches_oracle(k, n, count):
     f = fec(k, n)
@@ -510,6 +510,27 @@ def test_gpu_inversion_matches_oracle(k, n, count):
         er[list(lost)] = 1
         rows, cnt = f.pattern_rows(er.tobytes())
         assert cnt == len(lost)
+        got = np.frombuffer(rows, dtype=np.uint8).reshape(m, k)[:cnt]
+        assert (got == _host_rows(k, n, er)).all(), lost
+
+
+@pytest.mark.parametrize("k,n,count", [(10, 14, 0), (64, 80, 40), (17, 49, 30), (4, 6, 0)])
+def test_gpu_inversion_generic_matches_oracle(k, n, count, monkeypatch):
+    """The whole-matrix Gauss-Jordan path (RSMI_INVERT_GENERIC=1) gives the
+    same rows as the structured d x d path and the oracle."""
+    monkeypatch.setenv("RSMI_INVERT_GENERIC", "1")
+    f = rsmi.FEC(k, n)  # fresh ctx: patterns built under the knob
+    m = n - k
+    if count == 0:
+        pats = [c for e in range(1, m + 1) for c in itertools.combinations(range(n), e)]
+    else:
+        rng = np.random.default_rng(k * n)
+        pats = [tuple(sorted(rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)))
+                for _ in range(count)]
+    for lost in pats:
+        er = np.zeros(n, dtype=np.uint8)
+        er[list(lost)] = 1
+        rows, cnt = f.pattern_rows(er.tobytes())
         got = np.frombuffer(rows, dtype=np.uint8).reshape(m, k)[:cnt]
         assert (got == _host_rows(k, n, er)).all(), lost
 
