@@ -298,6 +298,8 @@ const Variant kVariants[] = {
     RS_VARIANT(10, 4, 256),   // RS(10,4): BASELINE configs 1-4
     RS_VARIANT(4, 4, 256),    // RS(4,2): plugin default (main.go:34-35)
     RS_VARIANT(8, 8, 256),    // infectious example RS(8,14)
+    RS_VARIANT(64, 4, 256),   // RS(64,16) reconstructs of <= 4 erasures (fewer VGPRs, smaller tables)
+    RS_VARIANT(64, 8, 256),   // ... and <= 8
     RS_VARIANT(64, 16, 256),  // RS(64,16): BASELINE config 5
     RS_VARIANT(0, 4, 256),
     RS_VARIANT(0, 8, 256),
@@ -309,7 +311,10 @@ const Variant kVariants[] = {
 #undef RS_VARIANT
 #undef RS_VARIANT_T
 
-const Variant& pick(int k, int m) {
+// The variant for a launch coding up to `rows` output rows per stripe: the
+// first specialised one for k whose row group holds them all (smaller row
+// groups are listed first), else row groups of the runtime-k kernels.
+const Variant& pick(int k, int rows) {
     static const int want_bt = [] {
         const char* e = std::getenv("RSMI_BLOCK");  // tuning knob
         return e ? std::atoi(e) : 256;
@@ -319,22 +324,23 @@ const Variant& pick(int k, int m) {
         return e ? std::atoi(e) != 0 : true;
     }();
     for (const Variant& v : kVariants)
-        if (v.K != 0 && v.K == k && m <= v.MG && v.BT == want_bt && v.nt == want_nt) return v;
+        if (v.K != 0 && v.K == k && rows <= v.MG && v.BT == want_bt && v.nt == want_nt) return v;
     for (const Variant& v : kVariants)
-        if (v.K != 0 && v.K == k && m <= v.MG && v.BT == want_bt) return v;
+        if (v.K != 0 && v.K == k && rows <= v.MG && v.BT == want_bt) return v;
     for (const Variant& v : kVariants)
-        if (v.K != 0 && v.K == k && m <= v.MG) return v;
-    if (k == 64) return kVariants[3];  // RS(64, m > 16): row groups of 16
-    return m <= 4 ? kVariants[4] : kVariants[5];
+        if (v.K != 0 && v.K == k && rows <= v.MG) return v;
+    for (const Variant& v : kVariants)
+        if (v.K == 64 && k == 64 && v.MG == 16) return v;  // RS(64, m > 16): row groups of 16
+    return rows <= 4 ? kVariants[6] : kVariants[7];
 }
 
 }  // namespace
 
-const char* variant_name(int k, int m) { return pick(k, m).name; }
+const char* variant_name(int k, int rows) { return pick(k, rows).name; }
 
 hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     if (a.stripes == 0 || a.ncols16 == 0 || max_e <= 0) return hipSuccess;
-    const Variant& v = pick(static_cast<int>(a.k), static_cast<int>(a.m));
+    const Variant& v = pick(static_cast<int>(a.k), max_e);
     const uint32_t total_it = (a.ncols16 + v.BT - 1) / v.BT;
     static const uint32_t iters_cap = [] {
         const char* e = std::getenv("RSMI_ITERS");  // tuning knob (default 1: one 4 KiB column chunk per block)

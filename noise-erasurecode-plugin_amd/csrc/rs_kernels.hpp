@@ -43,7 +43,7 @@ struct MatArgs {
 hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream);
 
 // Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
-const char* variant_name(int k, int m);
+const char* variant_name(int k, int rows);  // kernel coding up to `rows` outputs per stripe
 
 // splitmix64 byte stream fill (bench/test utility).
 hipError_t launch_fill_splitmix(void* dev, size_t len, uint64_t seed, hipStream_t stream);

@@ -597,7 +597,7 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         if (c->bitslice_rec)
             c->rec_name = c->bitslice_rec_min_e <= 1
                               ? std::string(c->bitslice->rec_name)
-                              : std::string(rsmi::variant_name(k, c->m)) + " (e<" +
+                              : std::string(rsmi::variant_name(k, std::min(c->m, c->bitslice_rec_min_e - 1))) + " (e<" +
                                     std::to_string(c->bitslice_rec_min_e) + ") + " + c->bitslice->rec_name;
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

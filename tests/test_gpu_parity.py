@@ -246,7 +246,7 @@ def _fec_env(k, n, **env):
 def test_bitslice_reconstruct_kernel_selection():
     """Batched reconstruct of a bit-sliced code goes through the generated
     syndrome kernel (bitslice.hpp) unless RSMI_BITSLICE_REC=0."""
-    assert fec(64, 80).kernel_name(1) == "K64_MG16_B256 (e<5) + bitslice_rec_k64_m16"
+    assert fec(64, 80).kernel_name(1) == "K64_MG4_B256 (e<5) + bitslice_rec_k64_m16"
     assert _fec_env(64, 80, RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == "bitslice_rec_k64_m16"
     assert _fec_env(64, 80, RSMI_BITSLICE_REC="0").kernel_name(1).startswith("K64_MG16")
     assert fec(10, 14).kernel_name(1).startswith("K10_MG4")
