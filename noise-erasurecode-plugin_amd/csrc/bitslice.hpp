@@ -53,6 +53,7 @@ struct BitsliceRecArgs {
     uint32_t dst_stride;
     uint32_t ncols16;
     uint32_t blocks_per_stripe;
+    const uint8_t* zpage;        // 2 KiB (one wave window) loaded for absent inputs
 };
 
 using BitsliceRecLaunch = hipError_t (*)(const BitsliceRecArgs&, hipStream_t);

@@ -323,6 +323,11 @@ void reset_patterns(rs_ctx* c) {
 }
 
 const uint8_t* dev_enc(rs_ctx* c) { return static_cast<const uint8_t*>(c->d_gf.p); }
+// 2 KiB of zeros: the address the bit-sliced reconstruct loads for absent
+// inputs (one wave's window, so those loads hit in L2 instead of HBM).
+const uint8_t* dev_zpage(rs_ctx* c) {
+    return static_cast<const uint8_t*>(c->d_gf.p) + round_up(static_cast<size_t>(c->n) * c->k + 768, 16) + 16;
+}
 uint32_t* dev_status(rs_ctx* c) {
     return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_gf.p) +
                                        round_up(static_cast<size_t>(c->n) * c->k + 768, 16));
@@ -614,7 +619,8 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     {
         const rsmi::Field& F = rsmi::field();
         const size_t nk = static_cast<size_t>(n) * k;
-        std::vector<uint8_t> gf(round_up(nk + 768, 16) + 16, 0);
+        // + status word, then a 2 KiB zero page (dev_zpage)
+        std::vector<uint8_t> gf(round_up(nk + 768, 16) + 16 + 2048, 0);
         std::copy(c->enc.begin(), c->enc.end(), gf.begin());
         std::memcpy(gf.data() + nk, F.exp, 510);
         std::memcpy(gf.data() + nk + 510, F.exp, 2);
@@ -845,6 +851,7 @@ static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, s
         b.dst_stride = a.dst_stride;
         b.ncols16 = a.ncols16;
         b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
+        b.zpage = dev_zpage(c);
         e = c->bitslice->reconstruct(b, s);
     }
     return hip_status(e);
