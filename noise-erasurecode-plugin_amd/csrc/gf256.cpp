@@ -108,9 +108,66 @@ std::vector<int> choose_survivors(const uint8_t* present, int k, int n) {
     return out;
 }
 
+// Rebuild-shaped survivor sets (every present data shard in its own slot,
+// the d erased data slots filled by parity shares): the rows follow from the
+// d x d inverse of B = enc[parity survivors][erased data] -- the same
+// construction as the GPU kernel (gf_invert.hip) and the same bytes as the
+// full inverse, which is unique.  Returns false if surv has another shape.
+static bool decode_rows_structured(const std::vector<uint8_t>& enc, int k, const std::vector<int>& surv,
+                                   const std::vector<int>& targets, std::vector<uint8_t>& rows, bool* singular) {
+    const Field& f = field();
+    std::vector<int> D, pos(k, -1);  // erased data slots; slot -> index in D
+    for (int i = 0; i < k; ++i) {
+        if (surv[i] == i) continue;
+        if (surv[i] < k) return false;
+        pos[i] = static_cast<int>(D.size());
+        D.push_back(i);
+    }
+    const int d = static_cast<int>(D.size());
+    std::vector<uint8_t> B(static_cast<size_t>(d) * d);
+    for (int a = 0; a < d; ++a)
+        for (int b = 0; b < d; ++b) B[a * d + b] = enc[static_cast<size_t>(surv[D[a]]) * k + D[b]];
+    if (d > 0 && !invert(B.data(), d)) {
+        *singular = true;
+        return true;
+    }
+    // G[b][j]: erased data D_b as a combination of the survivor slots
+    std::vector<uint8_t> G(static_cast<size_t>(d) * k, 0);
+    for (int b = 0; b < d; ++b)
+        for (int j = 0; j < k; ++j) {
+            if (pos[j] >= 0) {
+                G[b * k + j] = B[b * d + pos[j]];
+                continue;
+            }
+            uint8_t acc = 0;
+            for (int a = 0; a < d; ++a) acc ^= f.mul[B[b * d + a]][enc[static_cast<size_t>(surv[D[a]]) * k + j]];
+            G[b * k + j] = acc;
+        }
+    rows.assign(targets.size() * static_cast<size_t>(k), 0);
+    for (size_t t = 0; t < targets.size(); ++t) {
+        const int id = targets[t];
+        uint8_t* row = &rows[t * k];
+        if (id < k) {
+            if (pos[id] >= 0) std::memcpy(row, &G[static_cast<size_t>(pos[id]) * k], k);
+            else row[id] = 1;  // present in its own slot
+            continue;
+        }
+        const uint8_t* e = &enc[static_cast<size_t>(id) * k];
+        for (int j = 0; j < k; ++j) row[j] = pos[j] < 0 ? e[j] : 0;
+        for (int b = 0; b < d; ++b) {
+            const uint8_t c = e[D[b]];
+            if (!c) continue;
+            for (int j = 0; j < k; ++j) row[j] ^= f.mul[c][G[b * k + j]];
+        }
+    }
+    return true;
+}
+
 bool decode_rows(const std::vector<uint8_t>& enc, int k, int n, const std::vector<int>& surv,
                  const std::vector<int>& targets, std::vector<uint8_t>& rows) {
     (void)n;
+    bool singular = false;
+    if (decode_rows_structured(enc, k, surv, targets, rows, &singular)) return !singular;
     const Field& f = field();
     std::vector<uint8_t> M(static_cast<size_t>(k) * k);
     for (int i = 0; i < k; ++i) std::memcpy(&M[i * k], &enc[static_cast<size_t>(surv[i]) * k], k);
