@@ -357,6 +357,35 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     return hipGetLastError();
 }
 
+namespace {
+// One block per (piece, 4 KiB chunk): 256 lanes x 16 bytes.
+__global__ __launch_bounds__(256) void copy_pieces_kernel(const uint8_t* src, uint8_t* dst, const uint64_t* pieces,
+                                                          uint32_t chunks, uint32_t cols16) {
+    const uint32_t piece = blockIdx.x / chunks;
+    const uint32_t col = (blockIdx.x - piece * chunks) * 256u + threadIdx.x;
+    if (col >= cols16) return;
+    const uint64_t so = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pieces[2 * piece])) |
+                        (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pieces[2 * piece] >> 32))) << 32);
+    const uint64_t d0 = pieces[2 * piece + 1];
+    const uint64_t dof = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(d0)) |
+                         (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(d0 >> 32))) << 32);
+    const uint4 v = gload16<true>(src + so + static_cast<uint64_t>(col) * 16u);
+    gstore16<true>(dst + dof + static_cast<uint64_t>(col) * 16u, v);
+}
+}  // namespace
+
+hipError_t launch_copy_pieces(const uint8_t* src, uint8_t* dst, const uint64_t* pieces, uint32_t count,
+                              size_t bytes, hipStream_t stream) {
+    if (count == 0 || bytes == 0) return hipSuccess;
+    if (bytes % 16 != 0) return hipErrorInvalidValue;
+    const uint64_t cols16 = bytes / 16, chunks = (cols16 + 255) / 256;
+    if (cols16 > 0xFFFFFFFFull || static_cast<uint64_t>(count) * chunks > 0x7FFFFFFFull)
+        return hipErrorInvalidConfiguration;
+    hipLaunchKernelGGL(copy_pieces_kernel, dim3(static_cast<uint32_t>(count * chunks)), dim3(256), 0, stream, src, dst,
+                       pieces, static_cast<uint32_t>(chunks), static_cast<uint32_t>(cols16));
+    return hipGetLastError();
+}
+
 hipError_t launch_fill_splitmix(void* dev, size_t len, uint64_t seed, hipStream_t stream) {
     if (len == 0) return hipSuccess;
     const size_t nq = len / 8 + 1;

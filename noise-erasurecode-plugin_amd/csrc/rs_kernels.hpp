@@ -45,6 +45,13 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream);
 // Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
 const char* variant_name(int k, int rows);  // kernel coding up to `rows` outputs per stripe
 
+// Device-side copy of `count` pieces of `bytes` bytes (a multiple of 16):
+// piece i copies src + pieces[2i] to dst + pieces[2i+1] (16-byte aligned
+// offsets).  rs_decode_batch packs survivors / unpacks regenerated shards
+// with it so PCIe carries only those.
+hipError_t launch_copy_pieces(const uint8_t* src, uint8_t* dst, const uint64_t* pieces, uint32_t count,
+                              size_t bytes, hipStream_t stream);
+
 // splitmix64 byte stream fill (bench/test utility).
 hipError_t launch_fill_splitmix(void* dev, size_t len, uint64_t seed, hipStream_t stream);
 

@@ -152,9 +152,14 @@ struct rs_ctx {
     Staging st_stripe;   // stripe descriptors
     std::vector<uint32_t> scratch_pid, scratch_start;
 
-    // rs_decode_batch staging: pinned [batch][n][pitch] image and its device twin.
+    // rs_decode_batch: pinned staging of the packed survivors / regenerated
+    // shards, the device [batch][n][pitch] image, the packed device buffer and
+    // the copy-piece lists.
     Staging st_batch;
+    Staging st_pieces;
     DevBuf d_batch;
+    DevBuf d_pack;
+    DevBuf d_pieces;
     // Host-buffer API: pinned staging pipeline (created on first use) and the
     // device copy of a decode call's one-pattern table.
     std::unique_ptr<rsmi::HostPipeline> pipe;
@@ -982,39 +987,81 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
     }
     if (fast.empty()) return rc;
-    // 3. the rest: one reconstruct launch over [batch][n][pitch]
+    // 3. the rest: one reconstruct launch over a device [batch][n][pitch]
+    //    image.  PCIe carries only the k survivors of each message in (packed
+    //    [batch][k][pitch], scattered on the device) and only the regenerated
+    //    data shards out (gathered into [E][pitch]); present data shards go
+    //    from the caller's buffers to dst on the host.
     const size_t pitch = round_up(S, 256), stripe = pitch * static_cast<size_t>(n);
     const size_t B = fast.size();
+    std::vector<uint8_t> erased(B * static_cast<size_t>(n), 0);
+    std::vector<uint64_t> pin, pout;  // {src offset, dst offset} pairs
+    std::vector<rsmi::CopyPool::Piece> in, direct;
+    std::vector<std::pair<size_t, uint8_t*>> regen;  // packed index -> dst
+    pin.reserve(2 * B * k);
+    for (size_t j = 0; j < B; ++j) {
+        size_t q = 0;
+        for (int i = 0; i < n; ++i) {
+            const uint8_t* p = by[fast[j]][i];
+            if (!p) {
+                erased[j * n + i] = 1;
+                if (i < k) {
+                    pout.push_back(j * stripe + static_cast<size_t>(i) * pitch);
+                    pout.push_back(regen.size() * pitch);
+                    regen.push_back({regen.size(), dsts[fast[j]] + static_cast<size_t>(i) * S});
+                }
+                continue;
+            }
+            const size_t slot = j * k + q++;  // exactly k present (fast path)
+            pin.push_back(slot * pitch);
+            pin.push_back(j * stripe + static_cast<size_t>(i) * pitch);
+            if (i < k) direct.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, p, S});
+        }
+    }
+    const size_t E = regen.size();
+    const size_t packed = std::max(B * static_cast<size_t>(k), E) * pitch;
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
-    if (!c->st_batch.acquire(B * stripe) || !c->d_batch.reserve(B * stripe)) return RS_ENOMEM;
+    if (!c->pipe) return RS_ENOMEM;
+    const size_t piece_bytes = (pin.size() + pout.size()) * sizeof(uint64_t);
+    if (!c->st_batch.acquire(packed) || !c->d_batch.reserve(B * stripe) || !c->d_pack.reserve(packed) ||
+        !c->st_pieces.acquire(piece_bytes) || !c->d_pieces.reserve(piece_bytes))
+        return RS_ENOMEM;
     uint8_t* h = static_cast<uint8_t*>(c->st_batch.p);
-    std::vector<uint8_t> erased(B * static_cast<size_t>(n), 0);
-    std::vector<rsmi::CopyPool::Piece> in;
-    for (size_t j = 0; j < B; ++j)
-        for (int i = 0; i < n; ++i) {
-            const uint8_t* p = by[fast[j]][i];
-            if (p)
-                in.push_back({h + j * stripe + static_cast<size_t>(i) * pitch, p, S});
-            else
-                erased[j * n + i] = 1;
-        }
+    for (size_t j = 0; j < B; ++j) {
+        size_t q = 0;
+        for (int i = 0; i < n; ++i)
+            if (const uint8_t* p = by[fast[j]][i]) in.push_back({h + (j * k + q++) * pitch, p, S});
+    }
     c->pipe->copy(in);
+    uint64_t* hp = static_cast<uint64_t*>(c->st_pieces.p);
+    std::copy(pin.begin(), pin.end(), hp);
+    std::copy(pout.begin(), pout.end(), hp + pin.size());
     uint8_t* d = static_cast<uint8_t*>(c->d_batch.p);
+    uint8_t* dp = static_cast<uint8_t*>(c->d_pack.p);
+    const uint64_t* dpin = static_cast<const uint64_t*>(c->d_pieces.p);
     hipStream_t s = c->stream;
-    if (hipMemcpyAsync(d, h, B * stripe, hipMemcpyHostToDevice, s) != hipSuccess) return RS_EDEVICE;
+    const size_t sb = round_up(S, 16);
+    if (hipMemcpyAsync(c->d_pieces.p, hp, piece_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dp, h, B * k * pitch, hipMemcpyHostToDevice, s) != hipSuccess ||
+        rsmi::launch_copy_pieces(dp, d, dpin, static_cast<uint32_t>(pin.size() / 2), sb, s) != hipSuccess)
+        return RS_EDEVICE;
+    c->st_pieces.release_after(s);
     const int st = reconstruct_locked(c, d, stripe, d + pitch * k, stripe, pitch, S, B, erased.data(), s);
     if (st != RS_OK) return st;
-    if (hipMemcpy2DAsync(h, stripe, d, stripe, pitch * k, B, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+    if (E > 0 &&
+        (rsmi::launch_copy_pieces(d, dp, dpin + pin.size(), static_cast<uint32_t>(E), sb, s) != hipSuccess ||
+         hipMemcpyAsync(h, dp, E * pitch, hipMemcpyDeviceToHost, s) != hipSuccess))
         return RS_EDEVICE;
+    // present data shards need no GPU: copy them while the GPU works
+    c->pipe->copy(direct);
+    if (hipStreamSynchronize(s) != hipSuccess) return RS_EDEVICE;
     c->st_batch.release_after(s);
     std::vector<rsmi::CopyPool::Piece> out;
-    for (size_t j = 0; j < B; ++j)
-        for (int i = 0; i < k; ++i)
-            out.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, h + j * stripe + i * pitch, S});
+    out.reserve(E);
+    for (const auto& r : regen) out.push_back({r.second, h + r.first * pitch, S});
     c->pipe->copy(out);
     return rc;
 }
