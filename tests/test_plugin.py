@@ -206,6 +206,31 @@ def test_decode_batch_matches_decode():
     assert got == want
 
 
+@pytest.mark.parametrize("k,n,S", [(10, 14, 1000), (4, 6, 17), (64, 80, 4099)])
+def test_decode_batch_edge_sets(k, n, S):
+    """rs_decode_batch's packed transfers: messages with no erased data
+    (nothing regenerated: no gather), with every data shard erased, with only
+    data 0 / only data k-1 erased, a whole batch without regenerated data, and
+    ragged S (not a multiple of 16)."""
+    import rsmi
+    f = rsmi.NewFEC(k, n)
+    E = oracle.fec_matrix(k, n)
+    m = n - k
+    cases = [list(range(k)), list(range(m, n)), [i for i in range(n) if i != 0][:k],
+             [i for i in range(n) if i != k - 1][:k], list(range(1, k + 1))]
+    msgs, want = [], []
+    for b, keep in enumerate(cases):
+        data = oracle.splitmix_bytes(k * S, 900 + b).tobytes()
+        par = oracle.encode(E, k, n, data)
+        sh = [data[i * S:(i + 1) * S] for i in range(k)] + [par[i * S:(i + 1) * S] for i in range(m)]
+        msgs.append([rsmi.Share(i, sh[i]) for i in keep[::-1]])
+        want.append(data)
+    outs, st = f.DecodeBatch(msgs)
+    assert all(s == 0 for s in st) and outs == want
+    outs, st = f.DecodeBatch(msgs[:1] * 3)  # no message regenerates data
+    assert all(s == 0 for s in st) and outs == want[:1] * 3
+
+
 def test_receive_batch_equals_sequential_receive():
     k, n = 10, 14
     rng = np.random.default_rng(5)
