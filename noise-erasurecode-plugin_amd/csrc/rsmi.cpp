@@ -601,9 +601,12 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     c->bitslice = pick_bitslice(c->enc, k, c->m);
     c->bitslice_rec = pick_bitslice_rec(c->bitslice);
     {
-        // RS(64,16): the split-table kernel wins up to one 4-row group (e <= 4).
+        // RS(64,16): with the network restricted to the rows a pattern uses,
+        // the syndrome kernel beats the split-table kernel from e = 1
+        // (profiles/r01e_ab_minrec.log); a threshold > 1 sends stripes with
+        // fewer erasures to the split-table kernel.
         const char* ev = std::getenv("RSMI_BITSLICE_REC_MIN_E");
-        c->bitslice_rec_min_e = ev ? std::max(1, std::atoi(ev)) : 5;
+        c->bitslice_rec_min_e = ev ? std::max(1, std::atoi(ev)) : 1;
         if (c->bitslice_rec)
             c->rec_name = c->bitslice_rec_min_e <= 1
                               ? std::string(c->bitslice->rec_name)

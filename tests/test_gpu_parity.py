@@ -246,8 +246,9 @@ def _fec_env(k, n, **env):
 def test_bitslice_reconstruct_kernel_selection():
     """Batched reconstruct of a bit-sliced code goes through the generated
     syndrome kernel (bitslice.hpp) unless RSMI_BITSLICE_REC=0."""
-    assert fec(64, 80).kernel_name(1) == "K64_MG4_B256 (e<5) + bitslice_rec_k64_m16"
-    assert _fec_env(64, 80, RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == "bitslice_rec_k64_m16"
+    assert fec(64, 80).kernel_name(1) == "bitslice_rec_k64_m16"
+    assert _fec_env(64, 80, RSMI_BITSLICE_REC_MIN_E="5").kernel_name(1) == \
+        "K64_MG4_B256 (e<5) + bitslice_rec_k64_m16"
     assert _fec_env(64, 80, RSMI_BITSLICE_REC="0").kernel_name(1).startswith("K64_MG16")
     assert fec(10, 14).kernel_name(1).startswith("K10_MG4")
     assert _fec_env(10, 14, RSMI_BITSLICE="1", RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == \
@@ -302,11 +303,12 @@ def test_bitslice_reconstruct_roundtrip(k, n, S, pitch):
 
 
 def test_reconstruct_split_between_kernels():
-    """Default RS(64,16) reconstruct: stripes with e < 5 go to the split-table
-    kernel, the rest to the syndrome kernel, in one call (two launches)."""
+    """RS(64,16) reconstruct with RSMI_BITSLICE_REC_MIN_E=5: stripes with
+    e < 5 go to the split-table kernel, the rest to the syndrome kernel, in
+    one call (two launches)."""
     k, n, S = 64, 80, 8192
     m = n - k
-    f = fec(64, 80)
+    f = _fec_env(64, 80, RSMI_BITSLICE_REC_MIN_E="5")
     rng = np.random.default_rng(77)
     er = np.concatenate([_erasures(rng, 10, n, m, emin=1, emax=4),
                          _erasures(rng, 10, n, m, emin=5, emax=16)])
