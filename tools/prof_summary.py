@@ -146,9 +146,14 @@ def main():
         rec = [r for r in all_tr if "rs_bitslice_rec" in r["Kernel_Name"]]
         if rec:
             lines.append("")
-            lines.append(f"Reconstruct per step = the split-table launch (stripes with e < 5) plus the "
-                         f"syndrome launch; expected algorithmic bytes {st * (k + (m + 1) / 2) * S / 1e9:.2f} GB "
-                         f"(uniform 1..m erasures).")
+            split = any("rs_matmul_kernel" in r["Kernel_Name"] for r in all_tr)
+            what = ("the split-table launch (stripes with e below RSMI_BITSLICE_REC_MIN_E) plus the syndrome launch"
+                    if split else "one syndrome launch (every erasure count)")
+            rms = statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rec)
+            alg_rec = st * (k + (m + 1) / 2) * S
+            lines.append(f"Reconstruct per step = {what}; expected algorithmic bytes {alg_rec / 1e9:.2f} GB "
+                         f"(uniform 1..m erasures)" + ("." if split else
+                         f" / {rms:.3f} ms = **{alg_rec / (rms / 1e3) / 1e9:.0f} GB/s**."))
     rl = ["Per role (launch order alternates encode / reconstruct):"]
     rl.append("")
     rl.append("| role | launches | avg ms | grid (threads) | workgroup |")

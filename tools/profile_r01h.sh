@@ -1,0 +1,5 @@
+# r01h profiles: headline RS(10,4) (bench defaults) and BASELINE config 5
+# RS(64,16) 64 KiB shards (bit-sliced encode + bit-sliced syndrome reconstruct).
+set -o pipefail
+PROF_TAG=r01h bash tools/profile.sh || exit 1
+PROF_TAG=r01h_cfg5 PROF_ARGS="--k 64 --n 80 --shard 65536 --stripes 16384 --emax 16 --pattern-pool 256" bash tools/profile.sh || exit 1
