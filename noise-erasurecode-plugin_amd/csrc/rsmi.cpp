@@ -930,6 +930,11 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     return rebuild_into(c, present, by_id, share_len, dst);
 }
 
+// rs_decode_batch moves survivors in / regenerated shards out in up to
+// kBatchChunks pieces once a direction carries kBatchChunkMin bytes.
+constexpr size_t kBatchChunks = 4;
+constexpr size_t kBatchChunkMin = size_t(16) << 20;
+
 int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const uint8_t** shares,
                     size_t S, uint8_t** dsts, int* status) {
     if (!c || batch < 0 || (batch && (!counts || !numbers || !shares || !dsts || !status)))
@@ -1038,7 +1043,6 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         for (int i = 0; i < n; ++i)
             if (const uint8_t* p = by[fast[j]][i]) in.push_back({h + (j * k + q++) * pitch, p, S});
     }
-    c->pipe->copy(in);
     uint64_t* hp = static_cast<uint64_t*>(c->st_pieces.p);
     std::copy(pin.begin(), pin.end(), hp);
     std::copy(pout.begin(), pout.end(), hp + pin.size());
@@ -1047,26 +1051,55 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     const uint64_t* dpin = static_cast<const uint64_t*>(c->d_pieces.p);
     hipStream_t s = c->stream;
     const size_t sb = round_up(S, 16);
-    if (hipMemcpyAsync(c->d_pieces.p, hp, piece_bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dp, h, B * k * pitch, hipMemcpyHostToDevice, s) != hipSuccess ||
-        rsmi::launch_copy_pieces(dp, d, dpin, static_cast<uint32_t>(pin.size() / 2), sb, s) != hipSuccess)
+    if (hipMemcpyAsync(c->d_pieces.p, hp, piece_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return RS_EDEVICE;
+    // Survivors in, in chunks of messages: the host staging copy of chunk
+    // i + 1 runs while chunk i crosses PCIe (the staging buffer is pinned,
+    // so each hipMemcpyAsync returns at once).  `in` holds exactly k pieces
+    // per message, in message order.
+    const size_t chunks = std::min<size_t>(B, B * k * pitch >= kBatchChunkMin ? kBatchChunks : 1);
+    for (size_t ch = 0; ch < chunks; ++ch) {
+        const size_t j0 = B * ch / chunks, j1 = B * (ch + 1) / chunks;
+        c->pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
+        if (hipMemcpyAsync(dp + j0 * k * pitch, h + j0 * k * pitch, (j1 - j0) * k * pitch, hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+            return RS_EDEVICE;
+    }
+    if (rsmi::launch_copy_pieces(dp, d, dpin, static_cast<uint32_t>(pin.size() / 2), sb, s) != hipSuccess)
         return RS_EDEVICE;
     c->st_pieces.release_after(s);
     const int st = reconstruct_locked(c, d, stripe, d + pitch * k, stripe, pitch, S, B, erased.data(), s);
     if (st != RS_OK) return st;
-    if (E > 0 &&
-        (rsmi::launch_copy_pieces(d, dp, dpin + pin.size(), static_cast<uint32_t>(E), sb, s) != hipSuccess ||
-         hipMemcpyAsync(h, dp, E * pitch, hipMemcpyDeviceToHost, s) != hipSuccess))
-        return RS_EDEVICE;
+    // Regenerated data shards out, in chunks with an event each, so the host
+    // copies chunk i into the callers' buffers while chunk i + 1 crosses.
+    const size_t ochunks = E == 0 ? 0 : std::min<size_t>(E, E * pitch >= kBatchChunkMin ? kBatchChunks : 1);
+    hipEvent_t ev[kBatchChunks] = {};
+    int rc_dev = RS_OK;
+    if (E > 0 && rsmi::launch_copy_pieces(d, dp, dpin + pin.size(), static_cast<uint32_t>(E), sb, s) != hipSuccess)
+        rc_dev = RS_EDEVICE;
+    for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch) {
+        const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
+        if (hipMemcpyAsync(h + r0 * pitch, dp + r0 * pitch, (r1 - r0) * pitch, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[ch], hipEventDisableTiming) != hipSuccess || hipEventRecord(ev[ch], s) != hipSuccess)
+            rc_dev = RS_EDEVICE;
+    }
     // present data shards need no GPU: copy them while the GPU works
-    c->pipe->copy(direct);
+    if (rc_dev == RS_OK) c->pipe->copy(direct);
+    for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch) {
+        const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
+        if (hipEventSynchronize(ev[ch]) != hipSuccess) {
+            rc_dev = RS_EDEVICE;
+            break;
+        }
+        std::vector<rsmi::CopyPool::Piece> out;
+        out.reserve(r1 - r0);
+        for (size_t r = r0; r < r1; ++r) out.push_back({regen[r].second, h + regen[r].first * pitch, S});
+        c->pipe->copy(out);
+    }
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
     if (hipStreamSynchronize(s) != hipSuccess) return RS_EDEVICE;
     c->st_batch.release_after(s);
-    std::vector<rsmi::CopyPool::Piece> out;
-    out.reserve(E);
-    for (const auto& r : regen) out.push_back({r.second, h + r.first * pitch, S});
-    c->pipe->copy(out);
-    return rc;
+    return rc_dev != RS_OK ? rc_dev : rc;
 }
 
 void* rs_pinned_alloc(size_t bytes) {

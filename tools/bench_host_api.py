@@ -33,6 +33,8 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--batch-only", action="store_true", help="only the receive-batching section")
+    ap.add_argument("--batch-reps", type=int, default=3)
     a = ap.parse_args()
     import rsmi
     from rsmi import host as h
@@ -46,8 +48,9 @@ def main():
     f = rsmi.NewFEC(k, n)
     E = oracle.fec_matrix(k, n)
     P = ctypes.c_void_p
-    for name, size in (("config1_blob_1MiB+4", (1 << 20) + 4), ("msg_64KiB", 65540),
-                       ("msg_64MiB", 64 << 20), ("msg_640MiB", 640 << 20)):
+    sizes = (("config1_blob_1MiB+4", (1 << 20) + 4), ("msg_64KiB", 65540), ("msg_64MiB", 64 << 20),
+             ("msg_640MiB", 640 << 20))
+    for name, size in (() if a.batch_only else sizes):
         size -= size % k
         S = size // k
         blob = oracle.splitmix_bytes(size, 1)
@@ -102,7 +105,8 @@ def main():
             got.append(h.Share(int(s.ShardNumber), s.ShardData))
         msg, _ = hf.Decode(None, got)
         assert msg == blob
-    out["config1_plugin_end_to_end_ms"] = round(timeit(config1, a.reps) * 1e3, 3)
+    if not a.batch_only:
+        out["config1_plugin_end_to_end_ms"] = round(timeit(config1, a.reps) * 1e3, 3)
 
     # receive-side batching at the C ABI: B messages, each arriving with 4 of
     # its 14 shards lost -> B rs_decode calls vs one rs_decode_batch.
@@ -148,7 +152,7 @@ def main():
             assert rc == 0
 
         t_seq = timeit(seq, 3)
-        t_bat = timeit(bat, 3)
+        t_bat = timeit(bat, a.batch_reps)
         assert all((d == data).all() for d in dsts)
         out[label] = {"per_message_ms": round(t_seq / B * 1e3, 4),
                       "batched_ms_per_message": round(t_bat / B * 1e3, 4),
