@@ -231,6 +231,40 @@ def test_decode_batch_edge_sets(k, n, S):
     assert all(s == 0 for s in st) and outs == want[:1] * 3
 
 
+def test_decode_batch_chunked_transfers():
+    """A batch large enough that rs_decode_batch chunks both directions
+    (>= 16 MiB of survivors in and of regenerated data out): 25 messages of
+    ragged S = 262147, 3-4 data shards lost each (uneven chunk boundaries),
+    mixed with a Correct-path message and one without enough shares."""
+    import rsmi
+    k, n, S = 10, 14, 262147
+    m = n - k
+    B = 25
+    f = rsmi.NewFEC(k, n)
+    E = oracle.fec_matrix(k, n)
+    data = oracle.splitmix_bytes(B * k * S, 4242)
+    par = oracle.encode_batch(E, k, n, data, S, B)
+    rng = np.random.default_rng(11)
+    msgs, want = [], []
+    for b in range(B):
+        d = data[b * k * S:(b + 1) * k * S]
+        p = par[b * m * S:(b + 1) * m * S]
+        sh = [d[i * S:(i + 1) * S].tobytes() for i in range(k)] + [p[i * S:(i + 1) * S].tobytes() for i in range(m)]
+        lost = set(rng.choice(k, size=3 + b % 2, replace=False).tolist())
+        keep = [i for i in range(n) if i not in lost][:k]
+        if b == 7:
+            keep = [i for i in range(n) if i not in lost]  # k + 1 shares: Correct path
+        rng.shuffle(keep)
+        msgs.append([rsmi.Share(int(i), sh[i]) for i in keep])
+        want.append(d.tobytes())
+    msgs.insert(12, msgs[3][: k - 1])  # not enough shares
+    outs, st = f.DecodeBatch(msgs)
+    assert st[12] == rsmi.RS_ENOT_ENOUGH and outs[12] is None
+    del outs[12], st[12]
+    assert all(s == 0 for s in st)
+    assert outs == want
+
+
 def test_receive_batch_equals_sequential_receive():
     k, n = 10, 14
     rng = np.random.default_rng(5)
