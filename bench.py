@@ -127,8 +127,24 @@ def cpu_baseline(k, n, S, seconds, threads):
     }
 
 
+# The one JSON line goes to the real stdout; everything else written to fd 1
+# (RCCL's init banner, library prints) is sent to stderr so a driver reading
+# stdout sees only that line.
+_RESULT_OUT = None
+
+
+def emit(obj):
+    out = _RESULT_OUT or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def main():
+    global _RESULT_OUT
     args = parse()
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -281,7 +297,7 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     if distributed:
         torch.distributed.destroy_process_group()
 
@@ -352,7 +368,7 @@ def sharded_main(args, world, rank, local, dev, distributed):
     elapsed, rec_total, xgmi_total = (float(v) for v in vals.tolist())
     if rank == 0:
         xg = xgmi_total / elapsed / 1e9
-        print(json.dumps({
+        emit({
             "metric": "RS(10,4) reconstruct GB/s with RCCL survivor gather (configs[3], sharded)",
             "value": round(rec_total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -364,7 +380,7 @@ def sharded_main(args, world, rank, local, dev, distributed):
             "xgmi": {"gathered_GB": round(xgmi_total / 1e9, 3), "achieved_GBps_total": round(xg, 1),
                      "per_rank_GBps": round(xg / max(world, 1), 1),
                      "link_peak_GBps": 153.0, "links_per_gpu": 7},
-        }), flush=True)
+        })
     if distributed:
         torch.distributed.destroy_process_group()
 

@@ -117,6 +117,12 @@ def gather_survivors(held, plan: ExchangePlan, n: int, group=None):
     import torch.distributed as dist
 
     stripes, nloc, S = held.shape
+    if (nloc == n and len(plan.owned) == stripes and not any(len(r) for r in plan.send.values())
+            and not any(len(r) for r in plan.recv.values())
+            and np.array_equal(plan.local_src, plan.local_dst)):
+        # One rank holds and owns everything in the owner layout already
+        # (N = 1): the survivors are in place, nothing moves.
+        return held
     flat = held.reshape(stripes * nloc, S)
     out = torch.empty((len(plan.owned), n, S), dtype=held.dtype, device=held.device)
     oflat = out.view(len(plan.owned) * n, S)

@@ -119,3 +119,16 @@ def test_gather_and_reconstruct_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] == "ok" for r in res), res
+
+
+def test_gather_single_rank_in_place():
+    """N = 1: the holder buffer is already the owner layout, so the gather
+    moves nothing and returns it (the bench's sharded placement at N = 1)."""
+    E, full, er = dataset()
+    held = torch.from_numpy(np.ascontiguousarray(full[:, rd.local_shard_ids(0, N, 1), :]))
+    plan = rd.plan_exchange(er, K, N, 0, 1, S)
+    out = rd.gather_survivors(held, plan, N)
+    assert out.data_ptr() == held.data_ptr() and plan.bytes_in == 0
+    for j, s in enumerate(plan.owned):
+        for i in rd.choose_survivors(er[s], K, N):
+            assert (out[j, i].numpy() == full[s, i]).all()
