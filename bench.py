@@ -18,8 +18,9 @@ data path -> weak scaling.  The driver launches N>1 with torch.distributed.run.
 
 Also reported: the roofline of the dominant kernel (encode, HIP events on the
 launch stream) against the 8 TB/s HBM3E peak, and the CPU baseline (the
-oracle's AVX2 split-nibble port of infectious's addmul, on a bounded sample
-of the same workload, rank 0 at N=1 only).
+oracle's ports of infectious's scalar and split-nibble addmul, 1 thread and
+all usable CPUs, on a bounded sample of the same workload, rank 0 at N=1
+only).
 """
 from __future__ import annotations
 
@@ -62,7 +63,8 @@ def parse():
                     help="fixed erased shard ids for every stripe, e.g. 0,1,2,3 (default random)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU baseline sample (0 disables)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this job may use (affinity and cgroup quota)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -88,42 +90,92 @@ def pattern_total(n, emax):
     return sum(comb(n, e) for e in range(1, emax + 1))
 
 
-def cpu_baseline(k, n, S, seconds, threads):
-    """Oracle on a bounded sample of the same workload: batches of RS(k, n)
-    stripes with S-byte shards, each batch encoded (AVX2 split-nibble port of
-    infectious's addmul) and then reconstructed from 1..m random erasures
-    (Rebuild per stripe), `threads` pthreads over stripes; same algorithmic
-    byte accounting as the GPU line.  Runs until `seconds` have elapsed."""
-    from oracle import oracle
+def host_cpu_info():
+    """CPU model, the machine's logical CPUs, and the CPUs this process may
+    use (affinity mask, then the cgroup quota: the GPU box gives a job a
+    share of a large host)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    if quota:
+        usable = min(usable, quota)
+    return {"model": model, "host_cpus": total, "usable_cpus": usable, "cgroup_quota_cpus": quota}
 
+
+def _cpu_leg(oracle, E, k, n, S, seconds, threads, simd, rng):
+    """Encode + 1..m-erasure reconstruct batches of `threads` stripes for
+    `seconds`; returns (GB/s over algorithmic bytes, stripes, busy s)."""
     m = n - k
-    E = oracle.fec_matrix(k, n)
     batch = max(threads, 1)
     data = oracle.splitmix_bytes(batch * k * S, 0xC0FFEE)
-    parity = np.zeros(batch * m * S, dtype=np.uint8)
-    rng = np.random.default_rng(0xE4A5)
+    parity = np.ones(batch * m * S, dtype=np.uint8)  # touched: no page faults in the loop
     done_bytes = 0
     stripes_done = 0
     busy = 0.0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while busy < seconds:
         er = erasure_sets(rng, 1, batch, n, 1, m)[0]
         a = time.perf_counter()
-        parity[:] = oracle.encode_batch(E, k, n, data, S, batch, simd=True, threads=threads)
-        rc = oracle.reconstruct_batch(E, k, n, data, parity, S, batch, er, simd=True,
-                                      threads=threads)
+        oracle.encode_batch(E, k, n, data, S, batch, simd=simd, threads=threads, out=parity)
+        rc = oracle.reconstruct_batch(E, k, n, data, parity, S, batch, er, simd=simd, threads=threads)
         busy += time.perf_counter() - a
         assert rc == 0
         done_bytes += batch * (k + m) * S + int(((k + er.sum(axis=1)) * S).sum())
         stripes_done += batch
+    return done_bytes / busy / 1e9, stripes_done, busy
+
+
+def cpu_baseline(k, n, S, seconds, threads):
+    """The oracle (oracle/rs_oracle.c, a C restatement of infectious) on a
+    bounded sample of the same workload: batches of RS(k, n) stripes with
+    S-byte shards, each batch encoded and then reconstructed from 1..m random
+    erasures (Rebuild per stripe), pthreads over stripes, the GPU line's
+    algorithmic byte accounting.  Four legs share `seconds`: infectious's
+    generic scalar mul_table addmul and its amd64 split-nibble (PSHUFB, here
+    AVX2) addmul, each on 1 thread and on every CPU this job may use.
+    value = the all-CPU AVX2 leg."""
+    from oracle import oracle
+
+    info = host_cpu_info()
+    allc = threads or info["usable_cpus"]
+    E = oracle.fec_matrix(k, n)
+    rng = np.random.default_rng(0xE4A5)
+    legs = {}
+    samples = []
+    for name, simd, thr in (("scalar_1t", False, 1), ("scalar_all", False, allc),
+                            ("avx2_1t", True, 1), ("avx2_all", True, allc)):
+        gbps, st, busy = _cpu_leg(oracle, E, k, n, S, seconds / 4, thr, simd, rng)
+        legs[name] = {"GBps": round(gbps, 3), "threads": thr, "stripes": st, "seconds": round(busy, 2)}
+        samples.append(f"{name}: {st} stripes")
     return {
-        "value": round(done_bytes / busy / 1e9, 3),
+        "value": legs["avx2_all"]["GBps"],
         "unit": "GB/s",
-        "cores": threads,
+        "cores": allc,
         "kind": "port",
-        "sample": f"{stripes_done} RS({k},{n}) stripes of {S} B shards, encode + 1-{m}-erasure "
-                  f"reconstruct (oracle/rs_oracle.c, AVX2 split-nibble addmul), {threads} "
-                  f"threads, {busy:.1f} s",
+        "cpu_model": info["model"],
+        "host_cpus": info["host_cpus"],
+        "usable_cpus": info["usable_cpus"],
+        "cgroup_quota_cpus": info["cgroup_quota_cpus"],
+        "legs": legs,
+        "sample": f"RS({k},{n}) stripes of {S} B shards, encode + 1-{n - k}-erasure reconstruct "
+                  f"(oracle/rs_oracle.c: scalar mul_table and AVX2 split-nibble addmul), "
+                  f"1 thread and {allc} threads (all CPUs this job may use; the host has "
+                  f"{info['host_cpus']}): " + ", ".join(samples),
     }
 
 
@@ -251,8 +303,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(k, n, S, args.cpu_seconds, thr)
+            cpu = cpu_baseline(k, n, S, args.cpu_seconds, args.cpu_threads)
         out = {
             "metric": "RS(10,4) encode+reconstruct GB/s at 1/8 GPUs; % HBM roofline",
             "value": round(value, 2),

@@ -18,8 +18,14 @@
  *  - Host pointers are never retained past a call (cgo rule).
  *  - Device pointers / streams are HIP device pointers / hipStream_t passed
  *    as void*; the stream may be NULL (legacy default stream).
- *  - An rs_ctx is bound to one HIP device; calls on one ctx are serialised by
- *    an internal mutex, so a ctx may be shared between threads.
+ *  - An rs_ctx is bound to one HIP device and may be shared between threads
+ *    (noise calls Receive concurrently, once per peer connection,
+ *    main.go:49-52).  Each call leases its own stream, pinned staging and
+ *    device workspace from a pool inside the ctx (RSMI_MAX_LEASES, default
+ *    16, concurrent calls; more wait for a lease), so concurrent calls run
+ *    concurrently.  The only shared state is the decode-pattern cache,
+ *    guarded by a reader/writer lock: lookups and launches share it, only a
+ *    call that meets a new erasure pattern takes it exclusively.
  *  - There is no CPU fallback: without a usable gfx950 device rs_new returns
  *    RS_EDEVICE.
  */
@@ -134,8 +140,13 @@ int rs_reconstruct_stripes(rs_ctx *ctx, void *data, size_t data_stripe_stride,
                            size_t shard_len, size_t stripes, const uint8_t *erased,
                            void *stream);
 
-/* Cached decode patterns held by the ctx (diagnostics / tests). */
+/* Cached decode patterns held by the ctx (diagnostics / tests).  The cache
+ * holds at most 2^20 patterns (RSMI_PATTERN_CAP); a call that would exceed
+ * that evicts it whole, with no host synchronisation (the rebuilt rows wait
+ * on the device for the launches that read the old ones).
+ * rs_pattern_evictions counts those evictions. */
 int rs_pattern_count(const rs_ctx *ctx);
+int64_t rs_pattern_evictions(const rs_ctx *ctx);
 
 /* Diagnostics: the decode rows the engine uses for one erasure pattern
  * (erased = n flags).  rows receives m*k bytes: row t (t < *count) is the

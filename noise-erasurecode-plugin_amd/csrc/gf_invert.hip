@@ -24,6 +24,8 @@
 //    list is handled) and for A/B runs (InvertArgs::generic).
 #include "gf_invert.hpp"
 
+#include <atomic>
+
 namespace rsmi {
 namespace {
 
@@ -124,6 +126,7 @@ __global__ __launch_bounds__(kThreads) void invert_patterns_kernel(InvertArgs a)
     const uint32_t* tv = a.dst + static_cast<size_t>(p) * a.dst_stride;
     const int e = static_cast<int>(a.cnt[p]);
     uint8_t* out = a.coef + static_cast<size_t>(p) * m * k;
+    if (tid == 0) a.status[p] = 0u;  // set to 1 below if the survivor matrix is singular
 
     for (int i = tid; i < 512; i += kThreads) ex[i] = a.gf_exp[i];
     for (int i = tid; i < 256; i += kThreads) lg[i] = a.gf_log[i];
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(kThreads) void invert_patterns_kernel(InvertArgs a)
         }
         __syncthreads();
         if (!gj_invert(B, d, fac, swp, sh, gf)) {  // distinct survivors of an MDS code never are
-            if (tid == 0) atomicOr(a.status, 1u);
+            if (tid == 0) a.status[p] = 1u;
             return;
         }
         // G[b][j] = B^-1[b][pos j] for an erased slot j, else sum_a B^-1[b][a] F[a][j]
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void invert_patterns_kernel(InvertArgs a)
     }
     __syncthreads();
     if (!gj_invert(A, k, fac, swp, sh, gf)) {  // distinct survivors of an MDS code never are
-        if (tid == 0) atomicOr(a.status, 1u);
+        if (tid == 0) a.status[p] = 1u;
         return;
     }
     for (int t = wave; t < m; t += nwaves)
@@ -241,12 +244,12 @@ hipError_t launch_invert(const InvertArgs& a, uint32_t count, hipStream_t stream
     if (count == 0) return hipSuccess;
     const size_t lds = invert_lds_bytes(static_cast<int>(a.k), static_cast<int>(a.m));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set && lds > 65536) {
+    static std::atomic<bool> attr_set{false};  // contexts on several threads may launch
+    if (!attr_set.load() && lds > 65536) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(invert_patterns_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
-        attr_set = true;
+        attr_set.store(true);
     }
     hipLaunchKernelGGL(invert_patterns_kernel, dim3(count), dim3(kThreads), lds, stream, a);
     return hipGetLastError();

@@ -19,7 +19,7 @@ struct InvertArgs {
     uint8_t* coef;           // [npat][m][k] decode rows (output)
     uint32_t first;          // first pattern id to build
     uint32_t k, m;
-    uint32_t* status;        // bit 0 set if a survivor matrix was singular
+    uint32_t* status;        // [npat]: 1 if the pattern's survivor matrix is singular, else 0
     uint32_t generic;        // 1: whole k x k Gauss-Jordan even for Rebuild-shaped survivor sets (A/B)
 };
 

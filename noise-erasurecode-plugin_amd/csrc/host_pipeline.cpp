@@ -33,62 +33,71 @@ CopyPool::~CopyPool() {
     for (std::thread& t : threads_) t.join();
 }
 
+CopyPool& CopyPool::shared() {
+    // Leaked on purpose: worker threads must not be joined from a static
+    // destructor after the runtime has started tearing down.
+    static CopyPool* pool = new CopyPool(pool_threads());
+    return *pool;
+}
+
+bool CopyPool::claim(Job* j, Piece* out) {
+    if (j->next >= j->parts.size()) return false;
+    *out = j->parts[j->next++];
+    return true;
+}
+
 void CopyPool::worker() {
-    size_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
+        cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+        if (stop_) return;
+        Job* j = jobs_.front();
         Piece p{};
-        {
-            std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return stop_ || (generation_ != seen && next_ < work_.size()); });
-            if (stop_) return;
-            p = work_[next_++];
-            if (next_ == work_.size()) seen = generation_;
+        if (!claim(j, &p)) {  // every part handed out: the job leaves the queue
+            jobs_.pop_front();
+            continue;
         }
+        lk.unlock();
         std::memcpy(p.dst, p.src, p.len);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            if (++finished_ == work_.size()) done_cv_.notify_all();
-        }
+        lk.lock();
+        if (++j->finished == j->parts.size()) j->done_cv.notify_all();
     }
 }
 
 void CopyPool::run(const std::vector<Piece>& pieces) {
-    std::vector<Piece> parts;
+    Job job;
     for (const Piece& p : pieces)
         for (size_t o = 0; o < p.len; o += kPart)
-            parts.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o,
-                             std::min(kPart, p.len - o)});
-    if (parts.empty()) return;
-    if (threads_.empty() || parts.size() == 1) {
-        for (const Piece& p : parts) std::memcpy(p.dst, p.src, p.len);
+            job.parts.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o,
+                                 std::min(kPart, p.len - o)});
+    if (job.parts.empty()) return;
+    if (threads_.empty() || job.parts.size() == 1) {
+        for (const Piece& p : job.parts) std::memcpy(p.dst, p.src, p.len);
         return;
     }
-    {
-        std::lock_guard<std::mutex> lk(mu_);
-        work_ = std::move(parts);
-        next_ = 0;
-        finished_ = 0;
-        ++generation_;
-    }
-    cv_.notify_all();
-    // the calling thread helps
-    for (;;) {
-        Piece p{};
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            if (next_ >= work_.size()) break;
-            p = work_[next_++];
-        }
-        std::memcpy(p.dst, p.src, p.len);
-        std::lock_guard<std::mutex> lk(mu_);
-        if (++finished_ == work_.size()) done_cv_.notify_all();
-    }
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return finished_ == work_.size(); });
+    jobs_.push_back(&job);
+    cv_.notify_all();
+    // The calling thread works on its own job.  Workers only touch `job`
+    // under mu_ while it is queued or after claiming a part (finished <
+    // parts), so it may live on this stack.
+    Piece p{};
+    while (claim(&job, &p)) {
+        lk.unlock();
+        std::memcpy(p.dst, p.src, p.len);
+        lk.lock();
+        ++job.finished;
+    }
+    job.done_cv.wait(lk, [&] { return job.finished == job.parts.size(); });
+    for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
+        if (*it == &job) {
+            jobs_.erase(it);
+            break;
+        }
 }
 
 // -------------------------------------------------------- HostPipeline ----
-HostPipeline::HostPipeline() : pool_(pool_threads()) {}
+HostPipeline::HostPipeline() : pool_(CopyPool::shared()) {}
 
 HostPipeline::~HostPipeline() {
     for (Slot& s : slots_) {

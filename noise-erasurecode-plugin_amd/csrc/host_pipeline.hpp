@@ -4,15 +4,19 @@
 // (hipHostMalloc) staging in column chunks, with each chunk's H2D copy,
 // kernel and D2H copy on one of three HIP streams so that chunk c's GPU work
 // overlaps the staging copies of chunks c-1 and c+1.  Pageable <-> pinned
-// copies are split over a small worker pool.
+// copies are split over a process-wide worker pool.
+//
+// Every call on an rs_ctx leases its own HostPipeline (rsmi.cpp Lease), so
+// concurrent Receive goroutines (main.go:49-52) each stream through their
+// own slots; the copy pool takes jobs from any number of callers at once.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -20,7 +24,9 @@
 
 namespace rsmi {
 
-// Fixed set of worker threads running memcpy pieces.
+// Fixed set of worker threads running memcpy pieces for any number of
+// concurrent callers.  Each run() is a job; workers take parts from the
+// oldest unfinished job and the calling thread works on its own job.
 class CopyPool {
 public:
     explicit CopyPool(int threads);
@@ -32,14 +38,22 @@ public:
     };
     // Copies every piece (split further into <= 1 MiB parts); returns when done.
     void run(const std::vector<Piece>& pieces);
+    // The process-wide pool (RSMI_COPY_THREADS workers, default min(8, cpus)).
+    static CopyPool& shared();
 
 private:
+    struct Job {
+        std::vector<Piece> parts;
+        size_t next = 0, finished = 0;
+        std::condition_variable done_cv;
+    };
     void worker();
+    // Claims the next part of j (mu_ held); false once every part is claimed.
+    static bool claim(Job* j, Piece* out);
     std::vector<std::thread> threads_;
     std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    std::vector<Piece> work_;
-    size_t next_ = 0, finished_ = 0, generation_ = 0;
+    std::condition_variable cv_;
+    std::deque<Job*> jobs_;
     bool stop_ = false;
 };
 
@@ -56,7 +70,7 @@ public:
     hipError_t run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e, size_t S,
                    const ChunkLaunch& launch);
 
-    // Parallel pageable <-> pinned copies on the pipeline's worker pool.
+    // Parallel pageable <-> pinned copies on the shared worker pool.
     void copy(const std::vector<CopyPool::Piece>& pieces) { pool_.run(pieces); }
 
     static constexpr int kSlots = 3;
@@ -73,7 +87,7 @@ private:
     bool ensure(Slot& s, size_t in_bytes, size_t out_bytes);
     hipError_t drain(Slot& s, uint8_t* const* dsts, int e);
     Slot slots_[kSlots];
-    CopyPool pool_;
+    CopyPool& pool_;
 };
 
 }  // namespace rsmi

@@ -1,17 +1,22 @@
 // rsmi.cpp -- C ABI of the engine (include/rsmi.h).  Host-side bookkeeping
 // around the HIP kernels: encode/decode matrices, the per-ctx decode-pattern
-// cache, device workspaces and pinned staging.  The GF products themselves
-// always run on the GPU; there is no CPU compute fallback.
+// cache, and the per-call leases of streams, device workspaces and pinned
+// staging.  The GF products themselves always run on the GPU; there is no CPU
+// compute fallback.
 #include "../../include/rsmi.h"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -124,6 +129,66 @@ struct Staging {
 
 }  // namespace
 
+// rs_decode_batch moves survivors in / regenerated shards out in up to
+// kBatchChunks pieces once a direction carries kBatchChunkMin bytes.
+constexpr size_t kBatchChunks = 4;
+constexpr size_t kBatchChunkMin = size_t(16) << 20;
+
+namespace {
+
+// Per-call resources: every C-ABI call that needs a stream, staging or a
+// device workspace leases one of these from its ctx, so concurrent callers
+// (noise runs Receive once per peer connection, main.go:49-52) never share
+// them.  dev_done is recorded after the last GPU operation that reads the
+// lease's device buffers; the next user of the lease -- possibly on another
+// stream -- waits for it on the device (begin()), never on the host.
+struct Lease {
+    hipStream_t stream = nullptr;  // host API / decode_batch / pattern rows
+    hipEvent_t dev_done = nullptr;
+    std::atomic<bool> dev_pending{false};
+    hipEvent_t ev[kBatchChunks] = {};  // rs_decode_batch D2H chunk events
+    Staging st_stripe;                 // stripe descriptors
+    Staging st_batch, st_pieces;       // rs_decode_batch
+    DevBuf d_stripe_pat, d_batch, d_pack, d_pieces, d_onepat;
+    std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
+    std::vector<uint32_t> pid, start;          // reconstruct scratch
+
+    bool init() {
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+        if (hipEventCreateWithFlags(&dev_done, hipEventDisableTiming) != hipSuccess) return false;
+        for (hipEvent_t& e : ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+        return true;
+    }
+    // The next GPU use of the lease's device buffers, on stream s, follows
+    // the previous one (which may have been on another stream).
+    void begin(hipStream_t s) {
+        if (dev_pending.load()) (void)hipStreamWaitEvent(s, dev_done, 0);
+    }
+    void end(hipStream_t s) {
+        if (hipEventRecord(dev_done, s) == hipSuccess) dev_pending.store(true);
+    }
+    rsmi::HostPipeline* pipeline() {
+        if (!pipe) pipe.reset(new (std::nothrow) rsmi::HostPipeline());
+        return pipe.get();
+    }
+    ~Lease() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (dev_pending.load()) (void)hipEventSynchronize(dev_done);
+        pipe.reset();
+        st_stripe.destroy();
+        st_batch.destroy();
+        st_pieces.destroy();
+        for (DevBuf* b : {&d_stripe_pat, &d_batch, &d_pack, &d_pieces, &d_onepat}) b->release();
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (dev_done) (void)hipEventDestroy(dev_done);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+}  // namespace
+
 struct rs_ctx {
     int k = 0, n = 0, m = 0, device = 0;
     std::vector<uint8_t> enc;  // n x k systematic matrix
@@ -133,44 +198,75 @@ struct rs_ctx {
     bool bitslice_rec = false;  // batched reconstruct uses bitslice->reconstruct ...
     int bitslice_rec_min_e = 1;  // ... for stripes with at least this many erasures
     std::string rec_name;        // rs_kernel_name(ctx, 1) when bitslice_rec
-    std::mutex mu;
-    hipStream_t stream = nullptr;  // used by the host-buffer API
 
-    // Encode pattern on the device (PatBlob layout, one pattern).
+    // Immutable after rs_new: encode pattern (PatBlob layout, one pattern)
+    // and enc [n][k] | gf exp [512] | gf log [256] | 2 KiB zero page.
     DevBuf d_encpat;
+    DevBuf d_gf;
 
-    // Decode-pattern cache.  The host keeps each pattern's survivor / erased
-    // ids; the device holds the same plus its decode rows, which the GPU
-    // builds (gf_invert.hip) when a pattern is first seen.
+    // Decode-pattern cache, the only state calls share.  The host keeps each
+    // pattern's survivor / erased ids; the device holds the same plus its
+    // decode rows and status, which the GPU builds (gf_invert.hip) when a
+    // pattern is first seen.  Lookups and the launches that read the device
+    // tables hold pat_mu shared; creating patterns, growing the tables and
+    // eviction hold it exclusively.  pat_ev is recorded after every build
+    // (each build first waits for the previous one), so a launch on any
+    // stream that waits for it sees every row built so far.
+    mutable std::shared_mutex pat_mu;
     std::unordered_map<std::string, int> pat_index;
     std::vector<uint32_t> h_src, h_dst, h_cnt;  // [npat][k], [npat][dst_stride], [npat]
-    GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt;
-    size_t uploaded = 0;  // patterns built on the device
-    DevBuf d_gf;          // enc [n][k] | gf exp [512] | gf log [256] | status u32
-    DevBuf d_stripe_pat;
-    Staging st_pat;      // pattern-table uploads
-    Staging st_stripe;   // stripe descriptors
-    std::vector<uint32_t> scratch_pid, scratch_start;
+    GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat;
+    size_t uploaded = 0;    // patterns built on the device
+    size_t pat_cap = 0;     // soft bound; reaching it evicts the whole cache
+    uint64_t evictions = 0;
+    hipEvent_t pat_ev = nullptr;
+    bool pat_ev_valid = false;
+    Staging st_pat;  // pattern-table uploads
 
-    // rs_decode_batch: pinned staging of the packed survivors / regenerated
-    // shards, the device [batch][n][pitch] image, the packed device buffer and
-    // the copy-piece lists.
-    Staging st_batch;
-    Staging st_pieces;
-    DevBuf d_batch;
-    DevBuf d_pack;
-    DevBuf d_pieces;
-    // Host-buffer API: pinned staging pipeline (created on first use) and the
-    // device copy of a decode call's one-pattern table.
-    std::unique_ptr<rsmi::HostPipeline> pipe;
-    DevBuf d_work;
-    DevBuf d_onepat;
-    Staging st_one;
+    // Lease pool (FIFO: the least recently released lease is handed out).
+    std::mutex lease_mu;
+    std::condition_variable lease_cv;
+    std::vector<std::unique_ptr<Lease>> leases;
+    std::deque<Lease*> free_leases;
+    size_t max_leases = 16;
 };
+
 
 namespace {
 
 int hip_status(hipError_t e) { return e == hipSuccess ? RS_OK : RS_EDEVICE; }
+
+// ------------------------------------------------------------- leases ----
+Lease* acquire_lease(rs_ctx* c) {
+    std::unique_lock<std::mutex> lk(c->lease_mu);
+    c->lease_cv.wait(lk, [&] { return !c->free_leases.empty() || c->leases.size() < c->max_leases; });
+    if (!c->free_leases.empty()) {
+        Lease* L = c->free_leases.front();
+        c->free_leases.pop_front();
+        return L;
+    }
+    std::unique_ptr<Lease> L(new (std::nothrow) Lease());
+    if (!L || !L->init()) return nullptr;
+    c->leases.push_back(std::move(L));
+    return c->leases.back().get();
+}
+
+void release_lease(rs_ctx* c, Lease* L) {
+    {
+        std::lock_guard<std::mutex> lk(c->lease_mu);
+        c->free_leases.push_back(L);
+    }
+    c->lease_cv.notify_one();
+}
+
+struct LeaseGuard {
+    rs_ctx* c;
+    Lease* L;
+    explicit LeaseGuard(rs_ctx* ctx) : c(ctx), L(acquire_lease(ctx)) {}
+    ~LeaseGuard() {
+        if (L) release_lease(c, L);
+    }
+};
 
 // Output ids per pattern are padded to a multiple of 16 so the kernel can
 // load a whole row group's ids unconditionally.
@@ -232,7 +328,7 @@ bool check_stripes_args(const rs_ctx* c, const void* data, size_t dss, const voi
     return true;
 }
 
-rsmi::MatArgs base_args(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
+rsmi::MatArgs base_args(const rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
                         size_t pitch, size_t len, size_t stripes) {
     rsmi::MatArgs a{};
     a.data = static_cast<uint8_t*>(data);
@@ -263,7 +359,7 @@ const rsmi::BitsliceKernel* pick_bitslice(const std::vector<uint8_t>& enc, int k
 
 // Encode launch (all parity rows of every stripe): the generated bit-sliced
 // kernel when there is one for this code, else the split-table kernel.
-hipError_t launch_encode(rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s) {
+hipError_t launch_encode(const rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s) {
     if (!c->bitslice) return rsmi::launch_matmul(a, c->m, s);
     rsmi::BitsliceArgs b{};
     b.data = a.data;
@@ -289,22 +385,25 @@ bool pick_bitslice_rec(const rsmi::BitsliceKernel* b) {
     return b && b->reconstruct;
 }
 
-// Finds or creates the decode pattern for `erased` (n flags); -1 on error
-// with *err set.
-int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
+// ----------------------------------------------------- pattern cache ----
+std::string pattern_key(const rs_ctx* c, const uint8_t* erased, int* count) {
     std::string key(reinterpret_cast<const char*>(erased), static_cast<size_t>(c->n));
-    for (char& ch : key) ch = ch ? 1 : 0;
-    auto it = c->pat_index.find(key);
-    if (it != c->pat_index.end()) return it->second;
+    int e = 0;
+    for (char& ch : key) {
+        ch = ch ? 1 : 0;
+        e += ch;
+    }
+    *count = e;
+    return key;
+}
+
+// Creates the decode pattern for `key` (pat_mu held exclusively).
+int create_pattern(rs_ctx* c, std::string key) {
     std::vector<uint8_t> present(c->n);
     std::vector<int> targets;
     for (int i = 0; i < c->n; ++i) {
         present[i] = key[i] ? 0 : 1;
         if (key[i]) targets.push_back(i);
-    }
-    if (static_cast<int>(targets.size()) > c->m) {
-        *err = RS_ENOT_ENOUGH;
-        return -1;
     }
     std::vector<int> surv = rsmi::choose_survivors(present.data(), c->k, c->n);
     const int id = static_cast<int>(c->pat_index.size());
@@ -317,37 +416,73 @@ int pattern_for(rs_ctx* c, const uint8_t* erased, int* err) {
     return id;
 }
 
-// Drops the decode-pattern cache (bounded: pattern ids are 24 bits).
-void reset_patterns(rs_ctx* c) {
-    (void)hipDeviceSynchronize();
+// Pattern id of every stripe into pid.  With `create` (pat_mu exclusive)
+// missing patterns are added; without (pat_mu shared) they are counted in
+// *missing and their pid is left undefined.  More than m erasures in a
+// stripe -> RS_ENOT_ENOUGH.
+int lookup_patterns(rs_ctx* c, const uint8_t* erased, size_t stripes, std::vector<uint32_t>& pid,
+                    bool create, size_t* missing) {
+    pid.resize(stripes);
+    size_t miss = 0;
+    for (size_t i = 0; i < stripes; ++i) {
+        int e = 0;
+        std::string key = pattern_key(c, erased + i * c->n, &e);
+        if (e > c->m) return RS_ENOT_ENOUGH;
+        auto it = c->pat_index.find(key);
+        if (it != c->pat_index.end()) {
+            pid[i] = static_cast<uint32_t>(it->second);
+        } else if (create) {
+            pid[i] = static_cast<uint32_t>(create_pattern(c, std::move(key)));
+        } else {
+            ++miss;
+        }
+    }
+    if (missing) *missing = miss;
+    return RS_OK;
+}
+
+// Drops every cached pattern (pat_mu exclusive) without a host sync: the
+// next build, enqueued on s, waits on the device for the last launch of
+// every lease -- all launches that read the tables recorded their lease's
+// event while holding pat_mu -- before it overwrites rows.
+void evict_patterns(rs_ctx* c, hipStream_t s) {
+    {
+        std::lock_guard<std::mutex> lk(c->lease_mu);
+        for (const std::unique_ptr<Lease>& L : c->leases) L->begin(s);
+    }
     c->pat_index.clear();
     c->h_src.clear();
     c->h_dst.clear();
     c->h_cnt.clear();
     c->uploaded = 0;
+    ++c->evictions;
 }
 
-const uint8_t* dev_enc(rs_ctx* c) { return static_cast<const uint8_t*>(c->d_gf.p); }
+const uint8_t* dev_enc(const rs_ctx* c) { return static_cast<const uint8_t*>(c->d_gf.p); }
 // 2 KiB of zeros: the address the bit-sliced reconstruct loads for absent
 // inputs (one wave's window, so those loads hit in L2 instead of HBM).
-const uint8_t* dev_zpage(rs_ctx* c) {
-    return static_cast<const uint8_t*>(c->d_gf.p) + round_up(static_cast<size_t>(c->n) * c->k + 768, 16) + 16;
+const uint8_t* dev_zpage(const rs_ctx* c) {
+    return static_cast<const uint8_t*>(c->d_gf.p) + round_up(static_cast<size_t>(c->n) * c->k + 768, 16);
 }
-uint32_t* dev_status(rs_ctx* c) {
-    return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_gf.p) +
-                                       round_up(static_cast<size_t>(c->n) * c->k + 768, 16));
+
+// The stream s will read pattern rows: order it after every build so far.
+void wait_patterns(rs_ctx* c, hipStream_t s) {
+    if (c->pat_ev_valid) (void)hipStreamWaitEvent(s, c->pat_ev, 0);
 }
 
 // Uploads the ids of patterns created since the last flush and builds their
-// decode rows on the GPU (one workgroup per pattern), in stream order.
+// decode rows on the GPU (one workgroup per pattern), on stream s after the
+// previous build (pat_mu exclusive).
 int flush_patterns(rs_ctx* c, hipStream_t s) {
     const size_t npat = c->h_cnt.size(), first = c->uploaded;
     if (npat == first) return RS_OK;
+    wait_patterns(c, s);  // the growth copies below read rows an earlier build wrote
     const size_t k = c->k, m = c->m, ds = dst_stride(c);
     if (!c->d_pcoef.reserve_keep(npat * m * k, first * m * k, s) ||
         !c->d_psrc.reserve_keep(npat * k * 4, first * k * 4, s) ||
         !c->d_pdst.reserve_keep(npat * ds * 4, first * ds * 4, s) ||
-        !c->d_pcnt.reserve_keep(npat * 4, first * 4, s))
+        !c->d_pcnt.reserve_keep(npat * 4, first * 4, s) ||
+        !c->d_pstat.reserve_keep(npat * 4, first * 4, s))
         return RS_ENOMEM;
     const size_t cnt = npat - first;
     const size_t b_src = cnt * k * 4, b_dst = cnt * ds * 4, b_cnt = cnt * 4;
@@ -378,34 +513,136 @@ int flush_patterns(rs_ctx* c, hipStream_t s) {
     ia.first = static_cast<uint32_t>(first);
     ia.k = static_cast<uint32_t>(c->k);
     ia.m = static_cast<uint32_t>(c->m);
-    ia.status = dev_status(c);
+    ia.status = static_cast<uint32_t*>(c->d_pstat.p);
     {
         const char* g = std::getenv("RSMI_INVERT_GENERIC");
         ia.generic = g && std::atoi(g) != 0 ? 1u : 0u;
     }
     e = rsmi::launch_invert(ia, static_cast<uint32_t>(cnt), s);
     if (e != hipSuccess) return RS_EDEVICE;
+    if (hipEventRecord(c->pat_ev, s) != hipSuccess) return RS_EDEVICE;
+    c->pat_ev_valid = true;
     c->uploaded = npat;
     return RS_OK;
 }
 
-void set_cache_patterns(rs_ctx* c, rsmi::MatArgs& a) {
+void set_cache_patterns(const rs_ctx* c, rsmi::MatArgs& a) {
     a.coef = static_cast<const uint8_t*>(c->d_pcoef.p);
     a.src = static_cast<const uint32_t*>(c->d_psrc.p);
     a.dst = static_cast<const uint32_t*>(c->d_pdst.p);
     a.dst_stride = static_cast<uint32_t>(dst_stride(c));
 }
 
+// Launches the reconstruct of `stripes` whose patterns are in L.pid (pat_mu
+// held, shared or exclusive, and every pattern built): stripe descriptors
+// through L's staging and device buffer, then one launch per kernel.
+int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_t pss, size_t pitch,
+                       size_t len, size_t stripes, hipStream_t s) {
+    const std::vector<uint32_t>& pid = L.pid;
+    int max_e = 0;
+    for (size_t i = 0; i < stripes; ++i) max_e = std::max<int>(max_e, static_cast<int>(c->h_cnt[pid[i]]));
+    if (max_e == 0) return RS_OK;  // nothing erased anywhere
+    // Split between the kernels: with a bit-sliced reconstruct, stripes with
+    // few outputs may still go to the split-table kernel, whose cost grows
+    // with e while the syndrome network costs a whole encode
+    // (profiles/r01e_ab_minrec.log: the syndrome kernel wins from e = 1).
+    const int split_e = use_bitslice_rec(c) ? c->bitslice_rec_min_e : (c->m + 1);
+    auto high = [&](uint32_t p) { return static_cast<int>(c->h_cnt[p]) >= split_e; };
+    // Counting sort of the stripes by (kernel, pattern): each launch lists its
+    // stripes grouped by pattern (see rs_kernels.hpp stripe_desc).  The
+    // RSMI_NO_SORT knob keeps address order within a kernel (A/B runs).
+    static const bool no_sort = std::getenv("RSMI_NO_SORT") != nullptr;
+    const size_t npat = no_sort ? 1 : c->h_cnt.size();
+    const size_t nb = 2 * npat;
+    auto bucket = [&](size_t i) -> size_t { return (high(pid[i]) ? npat : 0) + (no_sort ? 0 : pid[i]); };
+    std::vector<uint32_t>& start = L.start;
+    start.assign(nb + 1, 0);
+    int max_lo = 0;
+    for (size_t i = 0; i < stripes; ++i) {
+        const uint32_t p = pid[i];
+        if (!c->h_cnt[p]) continue;  // stripes with nothing erased are skipped
+        ++start[bucket(i) + 1];
+        if (!high(p)) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
+    }
+    for (size_t b = 0; b < nb; ++b) start[b + 1] += start[b];
+    const size_t used = start[nb], n_lo = start[npat];
+    if (!L.st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
+    uint2* desc = static_cast<uint2*>(L.st_stripe.p);
+    for (size_t i = 0; i < stripes; ++i) {
+        const uint32_t p = pid[i];
+        if (c->h_cnt[p]) desc[start[bucket(i)]++] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
+    }
+    L.begin(s);  // the descriptor buffer's previous readers
+    wait_patterns(c, s);
+    if (!L.d_stripe_pat.reserve(used * sizeof(uint2))) return RS_ENOMEM;
+    hipError_t e = hipMemcpyAsync(L.d_stripe_pat.p, desc, used * sizeof(uint2), hipMemcpyHostToDevice, s);
+    L.st_stripe.release_after(s);
+    if (e != hipSuccess) return RS_EDEVICE;
+    const uint2* d_desc = static_cast<const uint2*>(L.d_stripe_pat.p);
+    if (n_lo > 0) {
+        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, n_lo);
+        set_cache_patterns(c, a);
+        a.stripe_desc = d_desc;
+        e = rsmi::launch_matmul(a, max_lo, s);
+    }
+    if (e == hipSuccess && used > n_lo) {
+        // Generated bit-sliced reconstruct (syndromes through the fixed
+        // encode network, bitslice.hpp): same descriptors and pattern cache.
+        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used - n_lo);
+        set_cache_patterns(c, a);
+        rsmi::BitsliceRecArgs b{};
+        b.data = a.data;
+        b.parity = a.parity;
+        b.data_ss = a.data_ss;
+        b.parity_ss = a.parity_ss;
+        b.pitch = a.pitch;
+        b.count = a.stripes;
+        b.stripe_desc = d_desc + n_lo;
+        b.coef = a.coef;
+        b.src = a.src;
+        b.dst = a.dst;
+        b.dst_stride = a.dst_stride;
+        b.ncols16 = a.ncols16;
+        b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
+        b.zpage = dev_zpage(c);
+        e = c->bitslice->reconstruct(b, s);
+    }
+    L.end(s);  // under pat_mu: an eviction waits for these launches
+    return hip_status(e);
+}
+
+// Batched reconstruct on stream s with lease L: lookups and launches under
+// a shared lock; only a call that meets new patterns takes it exclusively
+// (to create, build and, past the cap, evict).
+int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_t pss, size_t pitch,
+                size_t len, size_t stripes, const uint8_t* erased, hipStream_t s) {
+    size_t missing = 0;
+    {
+        std::shared_lock<std::shared_mutex> rl(c->pat_mu);
+        const int rc = lookup_patterns(c, erased, stripes, L.pid, false, &missing);
+        if (rc != RS_OK) return rc;
+        if (missing == 0) return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, s);
+    }
+    std::unique_lock<std::shared_mutex> wl(c->pat_mu);
+    if (c->pat_index.size() + missing > c->pat_cap) evict_patterns(c, s);
+    const int rc = lookup_patterns(c, erased, stripes, L.pid, true, nullptr);
+    if (rc != RS_OK) return rc;
+    if (c->pat_index.size() > (size_t(1) << 24)) return RS_EINVAL;  // 24-bit ids in the descriptors
+    const int st = flush_patterns(c, s);
+    if (st != RS_OK) return st;
+    return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, s);
+}
+
 // out_t = decode row (surv -> targets[t]) applied to the survivors, on the
-// GPU through the pinned host pipeline.  Caller holds c->mu on c->device.
-int gpu_rows(rs_ctx* c, const std::vector<int>& surv, const std::vector<const uint8_t*>& surv_ptr,
+// GPU through L's pinned host pipeline.  Runs on c->device.
+int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vector<const uint8_t*>& surv_ptr,
              const std::vector<int>& targets, const std::vector<uint8_t*>& outs, size_t S) {
     const int k = c->k, e = static_cast<int>(targets.size());
     if (e == 0 || S == 0) return RS_OK;
     std::vector<uint8_t> rows;
     if (!rsmi::decode_rows(c->enc, k, c->n, surv, targets, rows)) return RS_ESINGULAR;
-    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
-    if (!c->pipe) return RS_ENOMEM;
+    rsmi::HostPipeline* pipe = L.pipeline();
+    if (!pipe) return RS_ENOMEM;
     // A launch codes at most m rows per group of the one-pattern table; more
     // targets (possible when correcting) go in several passes.
     for (int t0 = 0; t0 < e; t0 += c->m) {
@@ -418,17 +655,19 @@ int gpu_rows(rs_ctx* c, const std::vector<int>& surv, const std::vector<const ui
         for (int t = 0; t < et; ++t) dstid[t] = static_cast<uint32_t>(k + t);
         std::vector<uint8_t> hp(PatLayout(c, 1).total);
         pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
-        if (!c->d_onepat.reserve(hp.size())) return RS_ENOMEM;
-        if (hipMemcpy(c->d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice) != hipSuccess)
+        // The previous pass's launches were drained by pipe->run.
+        if (!L.d_onepat.reserve(hp.size())) return RS_ENOMEM;
+        if (hipMemcpyAsync(L.d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice, L.stream) != hipSuccess ||
+            hipStreamSynchronize(L.stream) != hipSuccess)
             return RS_EDEVICE;
-        auto launch = [c, et](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
+        const void* pat = L.d_onepat.p;
+        auto launch = [c, et, pat](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
             rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
-            set_patterns(c, 1, c->d_onepat.p, a);
-            a.stripe_desc = first_stripe_desc(c, c->d_onepat.p);  // et outputs, not m
+            set_patterns(c, 1, pat, a);
+            a.stripe_desc = first_stripe_desc(c, pat);  // et outputs, not m
             return rsmi::launch_matmul(a, et, st);
         };
-        const hipError_t err =
-            c->pipe->run(surv_ptr.data(), k, outs.data() + t0, et, S, launch);
+        const hipError_t err = pipe->run(surv_ptr.data(), k, outs.data() + t0, et, S, launch);
         if (err != hipSuccess) return RS_EDEVICE;
     }
     return RS_OK;
@@ -436,7 +675,7 @@ int gpu_rows(rs_ctx* c, const std::vector<int>& surv, const std::vector<const ui
 
 // Rebuild from the present shares: data shares copied, missing ones
 // regenerated from Rebuild's survivors.
-int rebuild_into(rs_ctx* c, const std::vector<uint8_t>& present,
+int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
                  const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst) {
     const int k = c->k;
     std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
@@ -449,7 +688,7 @@ int rebuild_into(rs_ctx* c, const std::vector<uint8_t>& present,
             missing.push_back(i);
             outs.push_back(dst + static_cast<size_t>(i) * S);
         }
-    const int st = gpu_rows(c, surv, sp, missing, outs, S);
+    const int st = gpu_rows(c, L, surv, sp, missing, outs, S);
     if (st != RS_OK) return st;
     for (int i = 0; i < k; ++i)
         if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
@@ -480,8 +719,10 @@ std::vector<size_t> mismatched_columns(const std::vector<std::vector<uint8_t>>& 
 // work is GPU decodes; Berlekamp-Welch runs on the host for one column to
 // locate the bad shares, which are then treated as erasures, and again only
 // for columns that stay inconsistent.  Unlike infectious, the caller's share
-// bytes are not modified (the corrected values only land in dst).
-int correct_decode(rs_ctx* c, std::vector<uint8_t> present, const std::vector<const uint8_t*>& by_id,
+// bytes are not modified (the corrected values only land in dst).  The
+// result equals the oracle's Berlekamp-Welch restatement (oracle/rs_oracle.c
+// orc_bw_column); parity against upstream infectious is unpinned.
+int correct_decode(rs_ctx* c, Lease& L, std::vector<uint8_t> present, const std::vector<const uint8_t*>& by_id,
                    size_t S, uint8_t* dst) {
     const int k = c->k, n = c->n;
     std::vector<int> P;
@@ -504,10 +745,10 @@ int correct_decode(rs_ctx* c, std::vector<uint8_t> present, const std::vector<co
         po.push_back(pred[t].data());
         rx.push_back(by_id[extras[t]]);
     }
-    int st = gpu_rows(c, base, bp, extras, po, S);
+    int st = gpu_rows(c, L, base, bp, extras, po, S);
     if (st != RS_OK) return st;
     std::vector<size_t> bad = mismatched_columns(pred, rx, S);
-    if (bad.empty()) return rebuild_into(c, present, by_id, S, dst);
+    if (bad.empty()) return rebuild_into(c, L, present, by_id, S, dst);
     if ((r - k) / 2 <= 0) return RS_ENOT_ENOUGH;  // berlekampWelch: e <= 0
     // 2. locate the bad shares on the first inconsistent column
     std::vector<uint8_t> ys(r), cw(n);
@@ -541,7 +782,7 @@ int correct_decode(rs_ctx* c, std::vector<uint8_t> present, const std::vector<co
     }
     std::vector<const uint8_t*> bp2(k);
     for (int i = 0; i < k; ++i) bp2[i] = by_id[base2[i]];
-    st = gpu_rows(c, base2, bp2, targets, outs, S);
+    st = gpu_rows(c, L, base2, bp2, targets, outs, S);
     if (st != RS_OK) return st;
     for (int i = 0; i < k; ++i)
         if (in_b2[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
@@ -553,11 +794,22 @@ int correct_decode(rs_ctx* c, std::vector<uint8_t> present, const std::vector<co
     return RS_OK;
 }
 
-}  // namespace
+// Reads the status words of patterns [0, npat) after s has built them
+// (pat_mu held): RS_ESINGULAR if any survivor matrix was singular.
+int pattern_status(rs_ctx* c, size_t first, size_t count, hipStream_t s) {
+    if (count == 0) return RS_OK;
+    std::vector<uint32_t> st(count);
+    wait_patterns(c, s);
+    if (hipMemcpyAsync(st.data(), static_cast<uint32_t*>(c->d_pstat.p) + first, count * 4, hipMemcpyDeviceToHost,
+                       s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return RS_EDEVICE;
+    for (uint32_t v : st)
+        if (v) return RS_ESINGULAR;
+    return RS_OK;
+}
 
-static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss,
-                              size_t pitch, size_t len, size_t stripes, const uint8_t* erased,
-                              hipStream_t s);
+}  // namespace
 
 extern "C" {
 
@@ -613,7 +865,15 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
                               : std::string(rsmi::variant_name(k, std::min(c->m, c->bitslice_rec_min_e - 1))) + " (e<" +
                                     std::to_string(c->bitslice_rec_min_e) + ") + " + c->bitslice->rec_name;
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    {
+        // Pattern-cache bound (RSMI_PATTERN_CAP, for tests): 2^20 patterns,
+        // 1.3 GiB of tables for RS(64,16).
+        const char* pc = std::getenv("RSMI_PATTERN_CAP");
+        c->pat_cap = pc ? static_cast<size_t>(std::max(1, std::atoi(pc))) : (size_t(1) << 20);
+        const char* ml = std::getenv("RSMI_MAX_LEASES");
+        c->max_leases = ml ? static_cast<size_t>(std::max(1, std::atoi(ml))) : 16;
+    }
+    if (hipEventCreateWithFlags(&c->pat_ev, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return RS_EDEVICE;
     }
@@ -627,8 +887,8 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     {
         const rsmi::Field& F = rsmi::field();
         const size_t nk = static_cast<size_t>(n) * k;
-        // + status word, then a 2 KiB zero page (dev_zpage)
-        std::vector<uint8_t> gf(round_up(nk + 768, 16) + 16 + 2048, 0);
+        // then a 2 KiB zero page (dev_zpage)
+        std::vector<uint8_t> gf(round_up(nk + 768, 16) + 2048, 0);
         std::copy(c->enc.begin(), c->enc.end(), gf.begin());
         std::memcpy(gf.data() + nk, F.exp, 510);
         std::memcpy(gf.data() + nk + 510, F.exp, 2);
@@ -658,16 +918,13 @@ void rs_free(rs_ctx* c) {
     if (!c) return;
     {
         DeviceGuard g(c->device);
-        if (c->stream) (void)hipStreamSynchronize(c->stream);
         (void)hipDeviceSynchronize();
+        c->leases.clear();  // each lease syncs and frees its streams, staging and buffers
+        c->free_leases.clear();
         c->st_pat.destroy();
-        c->st_stripe.destroy();
-        c->st_one.destroy();
-        c->st_batch.destroy();
-        for (DevBuf* b : {&c->d_encpat, &c->d_stripe_pat, &c->d_work, &c->d_onepat, &c->d_gf, &c->d_batch})
-            b->release();
-        for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt}) b->release();
-        if (c->stream) (void)hipStreamDestroy(c->stream);
+        for (DevBuf* b : {&c->d_encpat, &c->d_gf}) b->release();
+        for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt, &c->d_pstat}) b->release();
+        if (c->pat_ev) (void)hipEventDestroy(c->pat_ev);
     }
     delete c;
 }
@@ -690,27 +947,38 @@ const char* rs_kernel_name(const rs_ctx* c, int which) {
 }
 
 int rs_pattern_count(const rs_ctx* c) {
-    return c ? static_cast<int>(c->pat_index.size()) : RS_EINVAL;
+    if (!c) return RS_EINVAL;
+    std::shared_lock<std::shared_mutex> rl(c->pat_mu);
+    return static_cast<int>(c->pat_index.size());
+}
+
+int64_t rs_pattern_evictions(const rs_ctx* c) {
+    if (!c) return RS_EINVAL;
+    std::shared_lock<std::shared_mutex> rl(c->pat_mu);
+    return static_cast<int64_t>(c->evictions);
 }
 
 int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count) {
     if (!c || !erased || !rows || !count) return RS_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    int err = RS_OK;
-    const int id = pattern_for(c, erased, &err);
-    if (id < 0) return err;
-    int st = flush_patterns(c, c->stream);
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    const hipStream_t s = lg.L->stream;
+    std::unique_lock<std::shared_mutex> wl(c->pat_mu);
+    std::vector<uint32_t> pid;
+    if (c->pat_index.size() + 1 > c->pat_cap) evict_patterns(c, s);
+    int st = lookup_patterns(c, erased, 1, pid, true, nullptr);
     if (st != RS_OK) return st;
-    const size_t mk = static_cast<size_t>(c->m) * c->k;
-    if (hipStreamSynchronize(c->stream) != hipSuccess ||
-        hipMemcpy(rows, static_cast<uint8_t*>(c->d_pcoef.p) + id * mk, mk, hipMemcpyDeviceToHost) != hipSuccess)
+    st = flush_patterns(c, s);
+    if (st != RS_OK) return st;
+    const size_t id = pid[0], mk = static_cast<size_t>(c->m) * c->k;
+    wait_patterns(c, s);
+    if (hipMemcpyAsync(rows, static_cast<uint8_t*>(c->d_pcoef.p) + id * mk, mk, hipMemcpyDeviceToHost, s) !=
+        hipSuccess)
         return RS_EDEVICE;
     *count = static_cast<int>(c->h_cnt[id]);
-    uint32_t status = 0;
-    if (hipMemcpy(&status, dev_status(c), 4, hipMemcpyDeviceToHost) != hipSuccess) return RS_EDEVICE;
-    return status ? RS_ESINGULAR : RS_OK;
+    return pattern_status(c, id, 1, s);  // synchronises s
 }
 
 int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
@@ -721,11 +989,14 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
         binom = binom * (c->n - e + 1) / e;
         total += binom;
     }
-    if (total > double(1 << 20)) return RS_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    if (total > double(1 << 20) || total > double(c->pat_cap)) return RS_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    std::unique_lock<std::shared_mutex> wl(c->pat_mu);
+    if (c->pat_index.size() + static_cast<size_t>(total) > c->pat_cap) evict_patterns(c, s);
     std::vector<uint8_t> er(c->n);
+    std::vector<uint32_t> pid;
     std::vector<int> idx;
     for (int e = 1; e <= max_e; ++e) {
         idx.resize(e);
@@ -733,8 +1004,8 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
         while (true) {
             std::fill(er.begin(), er.end(), 0);
             for (int v : idx) er[v] = 1;
-            int err = RS_OK;
-            if (pattern_for(c, er.data(), &err) < 0) return err;
+            const int err = lookup_patterns(c, er.data(), 1, pid, true, nullptr);
+            if (err != RS_OK) return err;
             int i = e - 1;
             while (i >= 0 && idx[i] == c->n - e + i) --i;
             if (i < 0) break;
@@ -742,12 +1013,9 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
             for (int j = i + 1; j < e; ++j) idx[j] = idx[j - 1] + 1;
         }
     }
-    int st = flush_patterns(c, static_cast<hipStream_t>(stream));
+    const int st = flush_patterns(c, s);
     if (st != RS_OK) return st;
-    if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return RS_EDEVICE;
-    uint32_t status = 0;
-    if (hipMemcpy(&status, dev_status(c), 4, hipMemcpyDeviceToHost) != hipSuccess) return RS_EDEVICE;
-    return status ? RS_ESINGULAR : RS_OK;
+    return pattern_status(c, 0, c->h_cnt.size(), s);  // synchronises s
 }
 
 int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, size_t pss,
@@ -755,7 +1023,7 @@ int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, siz
     if (!c) return RS_EINVAL;
     if (c->m == 0 || stripes == 0 || len == 0) return RS_OK;
     if (!check_stripes_args(c, data, dss, parity, pss, pitch, len)) return RS_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    // Reads only state that is immutable after rs_new: no lock, no lease.
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     rsmi::MatArgs a = base_args(c, const_cast<void*>(data), dss, parity, pss, pitch, len, stripes);
@@ -770,101 +1038,13 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     if (!c || !erased) return RS_EINVAL;
     if (stripes == 0 || len == 0) return RS_OK;
     if (!check_stripes_args(c, data, dss, parity, pss, pitch, len)) return RS_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    return reconstruct_locked(c, data, dss, parity, pss, pitch, len, stripes, erased,
-                              static_cast<hipStream_t>(stream));
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    return reconstruct(c, *lg.L, data, dss, parity, pss, pitch, len, stripes, erased,
+                       static_cast<hipStream_t>(stream));
 }
-
-}  // extern "C"
-
-static int reconstruct_locked(rs_ctx* c, void* data, size_t dss, void* parity, size_t pss, size_t pitch,
-                              size_t len, size_t stripes, const uint8_t* erased, hipStream_t s) {
-    if (c->pat_index.size() + stripes > (size_t(1) << 20)) reset_patterns(c);  // ids are 24-bit
-    // Pattern of every stripe, then a counting sort by pattern: the launch
-    // lists stripes grouped by pattern (see rs_kernels.hpp stripe_desc).
-    std::vector<uint32_t>& pid = c->scratch_pid;
-    pid.resize(stripes);
-    int max_e = 0;
-    for (size_t i = 0; i < stripes; ++i) {
-        int err = RS_OK;
-        const int id = pattern_for(c, erased + i * c->n, &err);
-        if (id < 0) return err;
-        pid[i] = static_cast<uint32_t>(id);
-        max_e = std::max<int>(max_e, static_cast<int>(c->h_cnt[id]));
-    }
-    if (max_e == 0) return RS_OK;  // nothing erased anywhere
-    // Split between the kernels: with a bit-sliced reconstruct, stripes with
-    // few outputs still go to the split-table kernel, whose cost grows with
-    // e while the syndrome network costs a whole encode (RS(64,16), one box:
-    // e=4 15.9 vs 18.6 ms, e=8 23.1 vs 20.0 ms; profiles/r01_ab_bitslice_rec.log).
-    const int split_e = use_bitslice_rec(c) ? c->bitslice_rec_min_e : (c->m + 1);
-    auto high = [&](uint32_t p) { return static_cast<int>(c->h_cnt[p]) >= split_e; };
-    // Counting sort of the stripes by (kernel, pattern): each launch lists its
-    // stripes grouped by pattern (see rs_kernels.hpp stripe_desc).  The
-    // RSMI_NO_SORT knob keeps address order within a kernel (A/B runs).
-    static const bool no_sort = std::getenv("RSMI_NO_SORT") != nullptr;
-    const size_t npat = no_sort ? 1 : c->h_cnt.size();
-    const size_t nb = 2 * npat;
-    auto bucket = [&](size_t i) -> size_t { return (high(pid[i]) ? npat : 0) + (no_sort ? 0 : pid[i]); };
-    std::vector<uint32_t>& start = c->scratch_start;
-    start.assign(nb + 1, 0);
-    int max_lo = 0;
-    for (size_t i = 0; i < stripes; ++i) {
-        const uint32_t p = pid[i];
-        if (!c->h_cnt[p]) continue;  // stripes with nothing erased are skipped
-        ++start[bucket(i) + 1];
-        if (!high(p)) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
-    }
-    for (size_t b = 0; b < nb; ++b) start[b + 1] += start[b];
-    const size_t used = start[nb], n_lo = start[npat];
-    if (!c->st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
-    uint2* desc = static_cast<uint2*>(c->st_stripe.p);
-    for (size_t i = 0; i < stripes; ++i) {
-        const uint32_t p = pid[i];
-        if (c->h_cnt[p]) desc[start[bucket(i)]++] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
-    }
-    int st = flush_patterns(c, s);
-    if (st != RS_OK) return st;
-    if (!c->d_stripe_pat.reserve(used * sizeof(uint2))) return RS_ENOMEM;
-    hipError_t e = hipMemcpyAsync(c->d_stripe_pat.p, desc, used * sizeof(uint2),
-                                  hipMemcpyHostToDevice, s);
-    c->st_stripe.release_after(s);
-    if (e != hipSuccess) return RS_EDEVICE;
-    const uint2* d_desc = static_cast<const uint2*>(c->d_stripe_pat.p);
-    if (n_lo > 0) {
-        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, n_lo);
-        set_cache_patterns(c, a);
-        a.stripe_desc = d_desc;
-        e = rsmi::launch_matmul(a, max_lo, s);
-        if (e != hipSuccess) return RS_EDEVICE;
-    }
-    if (used > n_lo) {
-        // Generated bit-sliced reconstruct (syndromes through the fixed
-        // encode network, bitslice.hpp): same descriptors and pattern cache.
-        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used - n_lo);
-        set_cache_patterns(c, a);
-        rsmi::BitsliceRecArgs b{};
-        b.data = a.data;
-        b.parity = a.parity;
-        b.data_ss = a.data_ss;
-        b.parity_ss = a.parity_ss;
-        b.pitch = a.pitch;
-        b.count = a.stripes;
-        b.stripe_desc = d_desc + n_lo;
-        b.coef = a.coef;
-        b.src = a.src;
-        b.dst = a.dst;
-        b.dst_stride = a.dst_stride;
-        b.ncols16 = a.ncols16;
-        b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
-        b.zpage = dev_zpage(c);
-        e = c->bitslice->reconstruct(b, s);
-    }
-    return hip_status(e);
-}
-extern "C" {
 
 int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     if (!c) return RS_EINVAL;
@@ -872,11 +1052,12 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     const size_t S = len / static_cast<size_t>(c->k);
     if (S == 0 || c->m == 0) return RS_OK;
     if (!input || !parity) return RS_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
-    if (!c->pipe) return RS_ENOMEM;
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    rsmi::HostPipeline* pipe = lg.L->pipeline();
+    if (!pipe) return RS_ENOMEM;
     std::vector<const uint8_t*> srcs(c->k);
     std::vector<uint8_t*> dsts(c->m);
     for (int j = 0; j < c->k; ++j) srcs[j] = input + static_cast<size_t>(j) * S;
@@ -886,7 +1067,7 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
         set_patterns(c, 1, c->d_encpat.p, a);
         return launch_encode(c, a, st);
     };
-    return hip_status(c->pipe->run(srcs.data(), c->k, dsts.data(), c->m, S, launch));
+    return hip_status(pipe->run(srcs.data(), c->k, dsts.data(), c->m, S, launch));
 }
 
 int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t share_len,
@@ -923,27 +1104,21 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (share_len == 0) return RS_OK;
     for (int i = 0; i < n; ++i)
         if (present[i] && !by_id[i]) return RS_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    if (distinct > k) return correct_decode(c, present, by_id, share_len, dst);
-    return rebuild_into(c, present, by_id, share_len, dst);
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    if (distinct > k) return correct_decode(c, *lg.L, present, by_id, share_len, dst);
+    return rebuild_into(c, *lg.L, present, by_id, share_len, dst);
 }
-
-// rs_decode_batch moves survivors in / regenerated shards out in up to
-// kBatchChunks pieces once a direction carries kBatchChunkMin bytes.
-constexpr size_t kBatchChunks = 4;
-constexpr size_t kBatchChunkMin = size_t(16) << 20;
 
 int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const uint8_t** shares,
                     size_t S, uint8_t** dsts, int* status) {
     if (!c || batch < 0 || (batch && (!counts || !numbers || !shares || !dsts || !status)))
         return RS_EINVAL;
     const int k = c->k, n = c->n;
-    // 1. validate + sort each message (rs_decode semantics); pick the ones
-    //    the batched path handles (exactly... at most k distinct shares is
-    //    impossible past validation, so: distinct == k, plus any count with
-    //    duplicates collapsing to k).
+    // 1. validate + sort each message (rs_decode semantics); messages with
+    //    exactly k distinct shares go to the batched launch.
     std::vector<size_t> first(batch + 1, 0);
     for (int b = 0; b < batch; ++b) first[b + 1] = first[b] + static_cast<size_t>(std::max(counts[b], 0));
     std::vector<int> fast;  // messages for the batched launch
@@ -1028,30 +1203,41 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     }
     const size_t E = regen.size();
     const size_t packed = std::max(B * static_cast<size_t>(k), E) * pitch;
-    std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
-    if (!c->pipe) c->pipe.reset(new (std::nothrow) rsmi::HostPipeline());
-    if (!c->pipe) return RS_ENOMEM;
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    Lease& L = *lg.L;
+    rsmi::HostPipeline* pipe = L.pipeline();
+    if (!pipe) return RS_ENOMEM;
+    const hipStream_t s = L.stream;
+    L.begin(s);  // the lease's buffers may last have been read on another stream
     const size_t piece_bytes = (pin.size() + pout.size()) * sizeof(uint64_t);
-    if (!c->st_batch.acquire(packed) || !c->d_batch.reserve(B * stripe) || !c->d_pack.reserve(packed) ||
-        !c->st_pieces.acquire(piece_bytes) || !c->d_pieces.reserve(piece_bytes))
+    if (!L.st_batch.acquire(packed) || !L.d_batch.reserve(B * stripe) || !L.d_pack.reserve(packed) ||
+        !L.st_pieces.acquire(piece_bytes) || !L.d_pieces.reserve(piece_bytes))
         return RS_ENOMEM;
-    uint8_t* h = static_cast<uint8_t*>(c->st_batch.p);
+    // From the first async copy on, every exit waits for the stream: the
+    // staging buffers may not be reused (or freed) while a DMA reads them.
+    auto finish = [&](int code) {
+        if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
+        L.end(s);
+        return code;
+    };
+    uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
     for (size_t j = 0; j < B; ++j) {
         size_t q = 0;
         for (int i = 0; i < n; ++i)
             if (const uint8_t* p = by[fast[j]][i]) in.push_back({h + (j * k + q++) * pitch, p, S});
     }
-    uint64_t* hp = static_cast<uint64_t*>(c->st_pieces.p);
+    uint64_t* hp = static_cast<uint64_t*>(L.st_pieces.p);
     std::copy(pin.begin(), pin.end(), hp);
     std::copy(pout.begin(), pout.end(), hp + pin.size());
-    uint8_t* d = static_cast<uint8_t*>(c->d_batch.p);
-    uint8_t* dp = static_cast<uint8_t*>(c->d_pack.p);
-    const uint64_t* dpin = static_cast<const uint64_t*>(c->d_pieces.p);
-    hipStream_t s = c->stream;
+    uint8_t* d = static_cast<uint8_t*>(L.d_batch.p);
+    uint8_t* dp = static_cast<uint8_t*>(L.d_pack.p);
+    const uint64_t* dpin = static_cast<const uint64_t*>(L.d_pieces.p);
     const size_t sb = round_up(S, 16);
-    if (hipMemcpyAsync(c->d_pieces.p, hp, piece_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return RS_EDEVICE;
+    if (hipMemcpyAsync(L.d_pieces.p, hp, piece_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+        return finish(RS_EDEVICE);
     // Survivors in, in chunks of messages: the host staging copy of chunk
     // i + 1 runs while chunk i crosses PCIe (the staging buffer is pinned,
     // so each hipMemcpyAsync returns at once).  `in` holds exactly k pieces
@@ -1059,47 +1245,43 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     const size_t chunks = std::min<size_t>(B, B * k * pitch >= kBatchChunkMin ? kBatchChunks : 1);
     for (size_t ch = 0; ch < chunks; ++ch) {
         const size_t j0 = B * ch / chunks, j1 = B * (ch + 1) / chunks;
-        c->pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
+        pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
         if (hipMemcpyAsync(dp + j0 * k * pitch, h + j0 * k * pitch, (j1 - j0) * k * pitch, hipMemcpyHostToDevice, s) !=
             hipSuccess)
-            return RS_EDEVICE;
+            return finish(RS_EDEVICE);
     }
     if (rsmi::launch_copy_pieces(dp, d, dpin, static_cast<uint32_t>(pin.size() / 2), sb, s) != hipSuccess)
-        return RS_EDEVICE;
-    c->st_pieces.release_after(s);
-    const int st = reconstruct_locked(c, d, stripe, d + pitch * k, stripe, pitch, S, B, erased.data(), s);
-    if (st != RS_OK) return st;
+        return finish(RS_EDEVICE);
+    const int st = reconstruct(c, L, d, stripe, d + pitch * k, stripe, pitch, S, B, erased.data(), s);
+    if (st != RS_OK) return finish(st);
     // Regenerated data shards out, in chunks with an event each, so the host
     // copies chunk i into the callers' buffers while chunk i + 1 crosses.
     const size_t ochunks = E == 0 ? 0 : std::min<size_t>(E, E * pitch >= kBatchChunkMin ? kBatchChunks : 1);
-    hipEvent_t ev[kBatchChunks] = {};
     int rc_dev = RS_OK;
     if (E > 0 && rsmi::launch_copy_pieces(d, dp, dpin + pin.size(), static_cast<uint32_t>(E), sb, s) != hipSuccess)
         rc_dev = RS_EDEVICE;
-    for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch) {
+    size_t queued = 0;
+    for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch, ++queued) {
         const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
         if (hipMemcpyAsync(h + r0 * pitch, dp + r0 * pitch, (r1 - r0) * pitch, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipEventCreateWithFlags(&ev[ch], hipEventDisableTiming) != hipSuccess || hipEventRecord(ev[ch], s) != hipSuccess)
+            hipEventRecord(L.ev[ch], s) != hipSuccess)
             rc_dev = RS_EDEVICE;
     }
     // present data shards need no GPU: copy them while the GPU works
-    if (rc_dev == RS_OK) c->pipe->copy(direct);
-    for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch) {
+    if (rc_dev == RS_OK) pipe->copy(direct);
+    for (size_t ch = 0; ch < queued && rc_dev == RS_OK; ++ch) {
         const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
-        if (hipEventSynchronize(ev[ch]) != hipSuccess) {
+        if (hipEventSynchronize(L.ev[ch]) != hipSuccess) {
             rc_dev = RS_EDEVICE;
             break;
         }
         std::vector<rsmi::CopyPool::Piece> out;
         out.reserve(r1 - r0);
         for (size_t r = r0; r < r1; ++r) out.push_back({regen[r].second, h + regen[r].first * pitch, S});
-        c->pipe->copy(out);
+        pipe->copy(out);
     }
-    for (hipEvent_t e : ev)
-        if (e) (void)hipEventDestroy(e);
-    if (hipStreamSynchronize(s) != hipSuccess) return RS_EDEVICE;
-    c->st_batch.release_after(s);
-    return rc_dev != RS_OK ? rc_dev : rc;
+    const int fin = finish(rc_dev);
+    return fin != RS_OK ? fin : rc;
 }
 
 void* rs_pinned_alloc(size_t bytes) {

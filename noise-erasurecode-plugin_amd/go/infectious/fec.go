@@ -152,9 +152,8 @@ func (f *FEC) Decode(dst []byte, shares []Share) ([]byte, error) {
 	} else {
 		dst = dst[:resultLen]
 	}
-	if pieceLen == 0 {
-		return dst, nil
-	}
+	// Zero-length shares still go through rs_decode, which validates the
+	// share numbers (invalid id, duplicates) exactly like Rebuild does.
 	cnt := len(shares)
 	nums := (*[1 << 28]C.int)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(C.int(0)))))[:cnt:cnt]
 	ptrs := (*[1 << 28]*C.uint8_t)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:cnt:cnt]
@@ -164,12 +163,19 @@ func (f *FEC) Decode(dst []byte, shares []Share) ([]byte, error) {
 	var pinner runtime.Pinner
 	defer pinner.Unpin()
 	for i := range shares {
-		pinner.Pin(&shares[i].Data[0])
 		nums[i] = C.int(shares[i].Number)
-		ptrs[i] = (*C.uint8_t)(unsafe.Pointer(&shares[i].Data[0]))
+		ptrs[i] = nil
+		if pieceLen > 0 {
+			pinner.Pin(&shares[i].Data[0])
+			ptrs[i] = (*C.uint8_t)(unsafe.Pointer(&shares[i].Data[0]))
+		}
+	}
+	var out *C.uint8_t
+	if resultLen > 0 {
+		out = (*C.uint8_t)(unsafe.Pointer(&dst[0]))
 	}
 	st := C.rs_decode(f.ctx, &nums[0], (**C.uint8_t)(unsafe.Pointer(&ptrs[0])), C.int(cnt),
-		C.size_t(pieceLen), (*C.uint8_t)(unsafe.Pointer(&dst[0])))
+		C.size_t(pieceLen), out)
 	if st != C.RS_OK {
 		return nil, statusErr(st)
 	}

@@ -36,7 +36,8 @@ RS_ETOO_MANY_ERRORS = -16
 EXPORTS = (
     "rs_new", "rs_new_on_device", "rs_free", "rs_k", "rs_n", "rs_device",
     "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode", "rs_decode_batch",
-    "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_prepare_patterns",
+    "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_pattern_evictions",
+    "rs_prepare_patterns",
     "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
     "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
@@ -86,6 +87,7 @@ def _lib() -> ctypes.CDLL:
             "rs_encode_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp]),
             "rs_reconstruct_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp, vp]),
             "rs_pattern_count": (i32, [vp]),
+            "rs_pattern_evictions": (ctypes.c_int64, [vp]),
             "rs_prepare_patterns": (i32, [vp, i32, vp]),
             "rs_pattern_rows": (i32, [vp, vp, vp, ctypes.POINTER(i32)]),
             "rs_pinned_alloc": (vp, [sz]),
@@ -271,6 +273,9 @@ class FEC:
 
     def pattern_count(self) -> int:
         return _lib().rs_pattern_count(self._h)
+
+    def pattern_evictions(self) -> int:
+        return _lib().rs_pattern_evictions(self._h)
 
     def pattern_rows(self, erased: bytes):
         """(rows bytes m*k, count) the engine uses for this erasure pattern."""

@@ -144,8 +144,11 @@ def matmul_stripe(coef: np.ndarray, shards: List[np.ndarray], simd: bool = False
 
 
 def encode_batch(enc: np.ndarray, k: int, n: int, data: np.ndarray, S: int, stripes: int,
-                 simd: bool = True, threads: int = 1) -> np.ndarray:
-    par = np.zeros(stripes * (n - k) * S, dtype=np.uint8)
+                 simd: bool = True, threads: int = 1, out: np.ndarray = None) -> np.ndarray:
+    """Parity of `stripes` stripes [stripes][k][S] -> [stripes][n-k][S], into
+    `out` when given (a pre-touched buffer keeps page faults, which
+    serialise threads, out of a timed loop)."""
+    par = np.zeros(stripes * (n - k) * S, dtype=np.uint8) if out is None else out
     lib().orc_encode_batch(_p(np.ascontiguousarray(enc)), k, n, _p(data), _p(par), S, stripes,
                            int(simd), threads)
     return par

@@ -460,6 +460,58 @@ def test_full_size_rs10_4_roundtrip():
     assert torch.equal(parity, p0)
 
 
+def test_config2_full_size_64GiB_roundtrip():
+    """The exact bench workload (BASELINE configs[1]+[2]): 6,553 RS(10,4)
+    stripes x 10 x 1 MiB = 64 GiB of data + 25.6 GiB of parity, offsets far
+    past 4 GiB.  Encode -> oracle spot checks of stripes whose bytes straddle
+    or lie beyond the 32-bit boundary in both regions -> erase 1-4 random
+    shards per stripe (bench.py's generator and seed) -> reconstruct ->
+    torch.equal of all 89.6 GiB against a device clone, plus the oracle's
+    Rebuild of the spot-checked stripes."""
+    import bench
+    k, n, S, stripes = 10, 14, 1 << 20, 6553
+    m = n - k
+    free, _ = torch.cuda.mem_get_info()
+    need = 2 * stripes * n * S + (1 << 30)
+    if free < need:
+        pytest.skip(f"needs {need >> 30} GiB free on the device")
+    f = fec(k, n)
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(data.data_ptr(), data.numel(), 0x5EED)
+    f.fill_splitmix(parity.data_ptr(), parity.numel(), 1)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    E = oracle.fec_matrix(k, n)
+    # 409: data straddles 2^32; 1023/1024: parity around 2^32; 3276 and the
+    # last stripe: data offsets ~34 GB and ~68.7 GB.
+    spots = (0, 409, 1023, 1024, 3276, stripes - 1)
+    assert 409 * k * S < (1 << 32) < 410 * k * S and 1024 * m * S == (1 << 32)
+    host = {}
+    for s in spots:
+        hd = data[s * k * S:(s + 1) * k * S].cpu().numpy().tobytes()
+        hp = parity[s * m * S:(s + 1) * m * S].cpu().numpy().tobytes()
+        assert hp == oracle.encode(E, k, n, hd), s
+        host[s] = [hd[i * S:(i + 1) * S] for i in range(k)] + [hp[i * S:(i + 1) * S] for i in range(m)]
+    d0, p0 = data.clone(), parity.clone()
+    rng = np.random.default_rng(0xE4A5)
+    er = bench.erasure_sets(rng, 1, stripes, n, 1, m)[0]
+    data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+    parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+    f.prepare_patterns(m)
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                          er.tobytes())
+    f.sync()
+    for s in spots:  # regenerated bytes vs the oracle's Rebuild of the same survivors
+        keep = [i for i in range(n) if not er[s, i]]
+        rc, ref = oracle.decode(E, k, n, [(i, host[s][i]) for i in keep[:k]])
+        assert rc == 0 and ref == data[s * k * S:(s + 1) * k * S].cpu().numpy().tobytes(), s
+    assert torch.equal(data, d0)
+    assert torch.equal(parity, p0)
+    del data, parity, d0, p0
+    torch.cuda.empty_cache()
+
+
 def test_distributed_owner_buffer_reconstruct_world1():
     """rsmi.distributed with G = 1: the owner buffer [owned, n, S] layout
     reconstructs in place through rs_reconstruct_stripes (the RCCL exchange
@@ -474,7 +526,7 @@ def test_distributed_owner_buffer_reconstruct_world1():
     er = _erasures(np.random.default_rng(9), stripes, n, n - k)
     plan = rd.plan_exchange(er, k, n, 0, 1, S)
     held = full.clone()
-    out = rd.gather_survivors(held, plan, n) if False else held  # G = 1: all local
+    out = rd.gather_survivors(held, plan, n)  # G = 1: every survivor is local
     bad = torch.from_numpy(er.astype(bool)).cuda()
     out[bad] = 0
     rd.reconstruct_owned(f, out, er)
