@@ -98,6 +98,8 @@ def _lib() -> ctypes.CDLL:
             "rs_fill_splitmix": (i32, [vp, vp, sz, ctypes.c_uint64, vp]),
         }
         for name, (res, args) in sig.items():
+            if os.environ.get("RSMI_LIB") and not hasattr(lib, name):
+                continue  # an older build selected for an A/B run
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
