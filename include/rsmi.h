@@ -161,6 +161,29 @@ int rs_pattern_rows(rs_ctx *ctx, const uint8_t *erased, uint8_t *rows, int *coun
  * index them.  RS_EINVAL if that would exceed 2^20 patterns. */
 int rs_prepare_patterns(rs_ctx *ctx, int max_erasures, void *stream);
 
+/* ---- signature hashing: batched BLAKE2b -----------
+ * The plugin signs and verifies blake2b(serializeMessage(id, message)):
+ * defaultHashPolicy = blake2b.New() (main.go:38-41), keys.Sign at
+ * main.go:219-223 on the send side, crypto.Verify at main.go:82-89 after
+ * every decode; the framing is serializeMessage (main.go:276-302).  These
+ * hash many messages per launch (RFC 7693 BLAKE2b, unkeyed, digest_len 1..64
+ * bytes; noise's policy is recalled to use the 32-byte digest, which is not
+ * BLAKE2b-512 truncated: the digest length is part of the parameter block).
+ * BLAKE2b chains a message's 128-byte blocks sequentially, so one message
+ * runs on 4 lanes; batches of hundreds of messages or more pay off.
+ *
+ * rs_blake2b_batch: host messages msgs[i] of lens[i] bytes (any alignment)
+ * -> out[i * digest_len ...].  Staged through pinned memory like
+ * rs_decode_batch; returns when out is written. */
+int rs_blake2b_batch(rs_ctx *ctx, int count, const uint8_t *const *msgs, const size_t *lens,
+                     int digest_len, uint8_t *out);
+/* rs_blake2b_device: device-resident messages.  msg_ptrs[count] (device
+ * addresses, any alignment) and lens[count] are device arrays; order
+ * (device, may be NULL) lists the messages longest first; out is device
+ * memory of count * digest_len bytes.  Enqueued on stream. */
+int rs_blake2b_device(rs_ctx *ctx, int count, const uint64_t *msg_ptrs, const uint64_t *lens,
+                      const uint32_t *order, int digest_len, uint8_t *out, void *stream);
+
 /* ---- memory helpers ------------------------------------------------------ */
 void *rs_pinned_alloc(size_t bytes); /* hipHostMalloc; NULL on failure */
 void rs_pinned_free(void *p);

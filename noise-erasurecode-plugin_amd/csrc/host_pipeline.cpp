@@ -9,6 +9,7 @@ namespace rsmi {
 
 namespace {
 constexpr size_t kPart = size_t(1) << 20;          // memcpy split granularity
+constexpr size_t kGroup = size_t(64) << 10;        // small pieces are handed out in runs of this many bytes
 constexpr size_t kChunkBytes = size_t(8) << 20;    // survivor bytes staged per chunk
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -40,10 +41,14 @@ CopyPool& CopyPool::shared() {
     return *pool;
 }
 
-bool CopyPool::claim(Job* j, Piece* out) {
-    if (j->next >= j->parts.size()) return false;
-    *out = j->parts[j->next++];
+bool CopyPool::claim(Job* j, size_t* part) {
+    if (j->next >= j->parts) return false;
+    *part = j->next++;
     return true;
+}
+
+void CopyPool::copy_part(const Job& j, size_t part) {
+    for (size_t i = j.bounds[part]; i < j.bounds[part + 1]; ++i) std::memcpy(j.pieces[i].dst, j.pieces[i].src, j.pieces[i].len);
 }
 
 void CopyPool::worker() {
@@ -52,27 +57,37 @@ void CopyPool::worker() {
         cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
         if (stop_) return;
         Job* j = jobs_.front();
-        Piece p{};
-        if (!claim(j, &p)) {  // every part handed out: the job leaves the queue
+        size_t part = 0;
+        if (!claim(j, &part)) {  // every part handed out: the job leaves the queue
             jobs_.pop_front();
             continue;
         }
         lk.unlock();
-        std::memcpy(p.dst, p.src, p.len);
+        copy_part(*j, part);
         lk.lock();
-        if (++j->finished == j->parts.size()) j->done_cv.notify_all();
+        if (++j->finished == j->parts) j->done_cv.notify_all();
     }
 }
 
 void CopyPool::run(const std::vector<Piece>& pieces) {
     Job job;
+    size_t group = 0;  // bytes in the part being grouped
+    job.bounds.push_back(0);
     for (const Piece& p : pieces)
-        for (size_t o = 0; o < p.len; o += kPart)
-            job.parts.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o,
-                                 std::min(kPart, p.len - o)});
-    if (job.parts.empty()) return;
-    if (threads_.empty() || job.parts.size() == 1) {
-        for (const Piece& p : job.parts) std::memcpy(p.dst, p.src, p.len);
+        for (size_t o = 0; o < p.len; o += kPart) {
+            const size_t len = std::min(kPart, p.len - o);
+            job.pieces.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o, len});
+            group += len;
+            if (group >= kGroup) {
+                job.bounds.push_back(job.pieces.size());
+                group = 0;
+            }
+        }
+    if (job.bounds.back() != job.pieces.size()) job.bounds.push_back(job.pieces.size());
+    job.parts = job.bounds.size() - 1;
+    if (job.parts == 0) return;
+    if (threads_.empty() || job.parts == 1) {
+        for (size_t i = 0; i < job.parts; ++i) copy_part(job, i);
         return;
     }
     std::unique_lock<std::mutex> lk(mu_);
@@ -81,14 +96,14 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
     // The calling thread works on its own job.  Workers only touch `job`
     // under mu_ while it is queued or after claiming a part (finished <
     // parts), so it may live on this stack.
-    Piece p{};
-    while (claim(&job, &p)) {
+    size_t part = 0;
+    while (claim(&job, &part)) {
         lk.unlock();
-        std::memcpy(p.dst, p.src, p.len);
+        copy_part(job, part);
         lk.lock();
         ++job.finished;
     }
-    job.done_cv.wait(lk, [&] { return job.finished == job.parts.size(); });
+    job.done_cv.wait(lk, [&] { return job.finished == job.parts; });
     for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
         if (*it == &job) {
             jobs_.erase(it);

@@ -42,14 +42,20 @@ public:
     static CopyPool& shared();
 
 private:
+    // A job's pieces, big ones split at 1 MiB, are handed out in parts:
+    // part i covers pieces [bounds[i], bounds[i + 1]) -- runs of small
+    // pieces are grouped so that thousands of small messages do not cost a
+    // lock round trip each.
     struct Job {
-        std::vector<Piece> parts;
-        size_t next = 0, finished = 0;
+        std::vector<Piece> pieces;
+        std::vector<size_t> bounds;
+        size_t next = 0, finished = 0, parts = 0;
         std::condition_variable done_cv;
     };
     void worker();
     // Claims the next part of j (mu_ held); false once every part is claimed.
-    static bool claim(Job* j, Piece* out);
+    static bool claim(Job* j, size_t* part);
+    static void copy_part(const Job& j, size_t part);
     std::vector<std::thread> threads_;
     std::mutex mu_;
     std::condition_variable cv_;

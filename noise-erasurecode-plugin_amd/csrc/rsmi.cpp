@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "bitslice.hpp"
+#include "blake2b.hpp"
 #include "gf256.hpp"
 #include "gf_invert.hpp"
 #include "host_pipeline.hpp"
@@ -1282,6 +1283,104 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     }
     const int fin = finish(rc_dev);
     return fin != RS_OK ? fin : rc;
+}
+
+int rs_blake2b_device(rs_ctx* c, int count, const uint64_t* msg_ptrs, const uint64_t* lens, const uint32_t* order,
+                      int digest_len, uint8_t* out, void* stream) {
+    if (!c || count < 0 || digest_len < 1 || digest_len > 64) return RS_EINVAL;
+    if (count == 0) return RS_OK;
+    if (!msg_ptrs || !lens || !out) return RS_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    rsmi::Blake2bArgs a{};
+    a.ptrs = msg_ptrs;
+    a.lens = lens;
+    a.order = order;
+    a.out = out;
+    a.count = static_cast<uint32_t>(count);
+    a.digest_len = static_cast<uint32_t>(digest_len);
+    return hip_status(rsmi::launch_blake2b(a, static_cast<hipStream_t>(stream)));
+}
+
+int rs_blake2b_batch(rs_ctx* c, int count, const uint8_t* const* msgs, const size_t* lens, int digest_len,
+                     uint8_t* out) {
+    if (!c || count < 0 || digest_len < 1 || digest_len > 64) return RS_EINVAL;
+    if (count == 0) return RS_OK;
+    if (!msgs || !lens || !out) return RS_EINVAL;
+    for (int i = 0; i < count; ++i)
+        if (!msgs[i] && lens[i]) return RS_EINVAL;
+    // Longest messages first: the quads of one wave then run about the same
+    // number of blocks.  Messages are packed 16-byte aligned in that order.
+    std::vector<uint32_t> order(count);
+    for (int i = 0; i < count; ++i) order[i] = static_cast<uint32_t>(i);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
+    std::vector<size_t> off(count);
+    size_t total = 0;
+    for (uint32_t i : order) {
+        off[i] = total;
+        total += round_up(lens[i], 16);
+    }
+    const size_t desc_bytes = round_up(static_cast<size_t>(count) * 20, 16);
+    const size_t dig_bytes = static_cast<size_t>(count) * digest_len;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    Lease& L = *lg.L;
+    rsmi::HostPipeline* pipe = L.pipeline();
+    if (!pipe) return RS_ENOMEM;
+    const hipStream_t s = L.stream;
+    L.begin(s);
+    if (!L.st_batch.acquire(std::max<size_t>(total, 16)) || !L.d_batch.reserve(std::max<size_t>(total, 16)) ||
+        !L.st_pieces.acquire(desc_bytes + dig_bytes) || !L.d_pieces.reserve(desc_bytes + dig_bytes))
+        return RS_ENOMEM;
+    auto finish = [&](int code) {
+        if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
+        L.end(s);
+        return code;
+    };
+    uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
+    uint8_t* d = static_cast<uint8_t*>(L.d_batch.p);
+    uint8_t* hd = static_cast<uint8_t*>(L.st_pieces.p);
+    uint8_t* dd = static_cast<uint8_t*>(L.d_pieces.p);
+    uint64_t* hptr = reinterpret_cast<uint64_t*>(hd);
+    uint64_t* hlen = hptr + count;
+    uint32_t* hord = reinterpret_cast<uint32_t*>(hlen + count);
+    for (int i = 0; i < count; ++i) {
+        hptr[i] = reinterpret_cast<uint64_t>(d + off[i]);
+        hlen[i] = lens[i];
+        hord[i] = order[i];
+    }
+    if (hipMemcpyAsync(dd, hd, desc_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return finish(RS_EDEVICE);
+    // Messages in, in up to kBatchChunks chunks (in packing order): the
+    // staging copy of chunk i + 1 overlaps the DMA of chunk i.
+    const size_t chunks = std::min<size_t>(count, total >= kBatchChunkMin ? kBatchChunks : 1);
+    for (size_t ch = 0; ch < chunks; ++ch) {
+        const size_t q0 = count * ch / chunks, q1 = count * (ch + 1) / chunks;
+        std::vector<rsmi::CopyPool::Piece> in;
+        for (size_t q = q0; q < q1; ++q)
+            if (lens[order[q]]) in.push_back({h + off[order[q]], msgs[order[q]], lens[order[q]]});
+        pipe->copy(in);
+        const size_t b0 = off[order[q0]];
+        const size_t b1 = q1 < static_cast<size_t>(count) ? off[order[q1]] : total;
+        if (b1 > b0 && hipMemcpyAsync(d + b0, h + b0, b1 - b0, hipMemcpyHostToDevice, s) != hipSuccess)
+            return finish(RS_EDEVICE);
+    }
+    rsmi::Blake2bArgs a{};
+    a.ptrs = reinterpret_cast<const uint64_t*>(dd);
+    a.lens = a.ptrs + count;
+    a.order = reinterpret_cast<const uint32_t*>(a.lens + count);
+    a.out = dd + desc_bytes;
+    a.count = static_cast<uint32_t>(count);
+    a.digest_len = static_cast<uint32_t>(digest_len);
+    if (rsmi::launch_blake2b(a, s) != hipSuccess) return finish(RS_EDEVICE);
+    if (hipMemcpyAsync(hd + desc_bytes, dd + desc_bytes, dig_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return finish(RS_EDEVICE);
+    const int rc = finish(RS_OK);
+    if (rc == RS_OK) std::memcpy(out, hd + desc_bytes, dig_bytes);
+    L.st_batch.release_after(s);
+    L.st_pieces.release_after(s);
+    return rc;
 }
 
 void* rs_pinned_alloc(size_t bytes) {

@@ -48,6 +48,7 @@ Status FEC::Encode(const uint8_t* input, size_t len,
         return from(RS_ELEN_NOT_MULTIPLE, "Encode");
     const size_t S = len / static_cast<size_t>(k_);
     const int m = n_ - k_;
+    std::lock_guard<std::mutex> lk(mu_);
     parity_.resize(static_cast<size_t>(m) * S);
     if (S && m) {
         const int rc = rs_encode(ctx_, input, len, parity_.data());

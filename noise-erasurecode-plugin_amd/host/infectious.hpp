@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -68,6 +69,7 @@ private:
     FEC(int k, int n, rs_ctx* c) : k_(k), n_(n), ctx_(c) {}
     int k_, n_;
     rs_ctx* ctx_;
+    std::mutex mu_;                // guards parity_ (a cached FEC is shared between threads)
     std::vector<uint8_t> parity_;  // reused between calls like infectious's fec_buf
 };
 

@@ -155,6 +155,30 @@ PYBIND11_MODULE(_rsmi_host, m) {
                  }
                  return out;
              })
+        .def("prepareShardsBatch",
+             [](ShardPlugin& p, const PeerID& self, const std::vector<py::bytes>& inputs) {
+                 std::vector<std::vector<uint8_t>> in;
+                 for (const py::bytes& b : inputs) in.push_back(to_vec(b));
+                 std::vector<std::vector<Shard>> out;
+                 std::vector<Status> sts;
+                 {
+                     py::gil_scoped_release nogil;
+                     p.prepareShardsBatch(self, in, &out, &sts);
+                 }
+                 std::vector<int> codes;
+                 for (const Status& s : sts) codes.push_back(s.code);
+                 return py::make_tuple(out, codes);
+             })
+        .def("HashBytes",
+             [](const ShardPlugin& p, const std::vector<py::bytes>& msgs) {
+                 std::vector<std::vector<uint8_t>> in, out;
+                 for (const py::bytes& b : msgs) in.push_back(to_vec(b));
+                 check(p.HashBytes(in, &out));
+                 py::list res;
+                 for (const auto& d : out) res.append(to_bytes(d));
+                 return res;
+             })
+        .def_readwrite("HashLen", &ShardPlugin::HashLen)
         .def("ShardAndBroadcast",
              [](ShardPlugin& p, const PeerID& self, const py::bytes& input,
                 const std::function<void(Shard)>& broadcast) {
@@ -171,7 +195,7 @@ PYBIND11_MODULE(_rsmi_host, m) {
 
     m.def("NewShardPlugin",
           [](std::function<py::bytes(py::bytes)> sign, std::function<bool(py::bytes, py::bytes)> verify,
-             int k, int n) {
+             int k, int n, int hash_len) {
               Signer s = [sign](const std::vector<uint8_t>& msg) {
                   py::gil_scoped_acquire g;
                   return to_vec(sign(to_bytes(msg)));
@@ -180,8 +204,9 @@ PYBIND11_MODULE(_rsmi_host, m) {
                   py::gil_scoped_acquire g;
                   return verify(to_bytes(msg), to_bytes(sig));
               };
-              return NewShardPlugin(s, v, k, n).release();
+              return NewShardPlugin(s, v, k, n, hash_len).release();
           },
+          py::arg("sign"), py::arg("verify"), py::arg("k"), py::arg("n"), py::arg("hash_len") = 0,
           py::return_value_policy::take_ownership);
     m.def("serializeMessage", [](const PeerID& id, const py::bytes& msg) {
         return to_bytes(serializeMessage(id, to_vec(msg)));

@@ -96,11 +96,38 @@ std::string HexString(const std::vector<uint8_t>& b) {
 }
 
 // ----------------------------------------------------------- ShardPlugin ---
-ShardPlugin::ShardPlugin(int k, int n, Signer sign, Verifier verify)
-    : MinimumNeededShards(k), TotalShards(n), sign_(std::move(sign)), verify_(std::move(verify)) {}
+ShardPlugin::ShardPlugin(int k, int n, Signer sign, Verifier verify, int hashLen)
+    : MinimumNeededShards(k), TotalShards(n), HashLen(hashLen), sign_(std::move(sign)), verify_(std::move(verify)) {}
 
-std::unique_ptr<ShardPlugin> NewShardPlugin(Signer sign, Verifier verify, int k, int n) {
-    return std::make_unique<ShardPlugin>(k, n, std::move(sign), std::move(verify));
+std::unique_ptr<ShardPlugin> NewShardPlugin(Signer sign, Verifier verify, int k, int n, int hashLen) {
+    return std::make_unique<ShardPlugin>(k, n, std::move(sign), std::move(verify), hashLen);
+}
+
+Status ShardPlugin::HashBytes(const std::vector<std::vector<uint8_t>>& msgs,
+                              std::vector<std::vector<uint8_t>>* out) const {
+    if (HashLen <= 0) {
+        *out = msgs;
+        return Status::Ok();
+    }
+    out->assign(msgs.size(), std::vector<uint8_t>(static_cast<size_t>(HashLen)));
+    if (msgs.empty()) return Status::Ok();
+    // Any context on the device serves the hash; use this plugin's code.
+    std::shared_ptr<FEC> f;
+    Status st = CachedFEC(MinimumNeededShards, TotalShards, &f);
+    if (!st.ok()) return st;
+    std::vector<const uint8_t*> ptrs(msgs.size());
+    std::vector<size_t> lens(msgs.size());
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        ptrs[i] = msgs[i].data();
+        lens[i] = msgs[i].size();
+    }
+    std::vector<uint8_t> dig(msgs.size() * static_cast<size_t>(HashLen));
+    const int rc = rs_blake2b_batch(f->ctx(), static_cast<int>(msgs.size()), ptrs.data(), lens.data(), HashLen,
+                                    dig.data());
+    if (rc != RS_OK) return Status::Err(rc, std::string("blake2b: ") + rs_strerror(rc));
+    for (size_t i = 0; i < msgs.size(); ++i)
+        std::copy(dig.begin() + i * HashLen, dig.begin() + (i + 1) * HashLen, (*out)[i].begin());
+    return Status::Ok();
 }
 
 size_t ShardPlugin::PoolSize(const std::vector<uint8_t>& sig) const {
@@ -125,8 +152,13 @@ Status ShardPlugin::shardInput(const std::vector<uint8_t>& input, std::vector<Sh
 Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
                                   std::vector<Shard>* out) {
     if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
-    const std::vector<uint8_t> sig = sign_ ? sign_(serializeMessage(self, *input))
-                                           : std::vector<uint8_t>();
+    std::vector<uint8_t> sig;
+    if (sign_) {
+        std::vector<std::vector<uint8_t>> h;
+        Status hs = HashBytes({serializeMessage(self, *input)}, &h);
+        if (!hs.ok()) return hs;
+        sig = sign_(h[0]);
+    }
     std::vector<Share> shares;
     Status st = shardInput(*input, &shares);
     if (!st.ok()) return st;
@@ -141,6 +173,41 @@ Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>
         out->push_back(std::move(m));
     }
     return Status::Ok();
+}
+
+void ShardPlugin::prepareShardsBatch(const PeerID& self, const std::vector<std::vector<uint8_t>>& inputs,
+                                     std::vector<std::vector<Shard>>* out, std::vector<Status>* sts) {
+    out->assign(inputs.size(), {});
+    sts->assign(inputs.size(), Status::Ok());
+    std::vector<std::vector<uint8_t>> sigs(inputs.size());
+    if (sign_) {
+        std::vector<std::vector<uint8_t>> ser, h;
+        ser.reserve(inputs.size());
+        for (const std::vector<uint8_t>& in : inputs) ser.push_back(serializeMessage(self, in));
+        Status hs = HashBytes(ser, &h);
+        if (!hs.ok()) {
+            sts->assign(inputs.size(), hs);
+            return;
+        }
+        for (size_t i = 0; i < inputs.size(); ++i) sigs[i] = sign_(h[i]);
+    }
+    for (size_t i = 0; i < inputs.size(); ++i) {
+        std::vector<Share> shares;
+        Status st = shardInput(inputs[i], &shares);
+        if (!st.ok()) {
+            (*sts)[i] = st;
+            continue;
+        }
+        for (Share& s : shares) {
+            Shard m;
+            m.FileSignature = sigs[i];
+            m.ShardData = std::move(s.Data);
+            m.ShardNumber = static_cast<uint64_t>(s.Number);
+            m.TotalShards = static_cast<uint64_t>(TotalShards);
+            m.MinimumNeededShards = static_cast<uint64_t>(MinimumNeededShards);
+            (*out)[i].push_back(std::move(m));
+        }
+    }
 }
 
 Status ShardPlugin::ShardAndBroadcast(const PeerID& self, const std::vector<uint8_t>* input,
@@ -185,8 +252,10 @@ Status ShardPlugin::Receive(const PeerID& sender, const Shard& msg, ReceiveEvent
                                 static_cast<int>(msg.TotalShards), &f);
     if (e.decode_status.ok()) e.decode_status = f->Decode(&e.message, pool);
     if (!e.decode_status.ok()) e.message.clear();
-    e.verified = e.decode_status.ok() && verify_ &&
-                 verify_(serializeMessage(sender, e.message), msg.FileSignature);
+    if (e.decode_status.ok() && verify_) {
+        std::vector<std::vector<uint8_t>> h;
+        if (HashBytes({serializeMessage(sender, e.message)}, &h).ok()) e.verified = verify_(h[0], msg.FileSignature);
+    }
     if (e.verified) {  // main.go:90-92
         std::lock_guard<std::mutex> lk(mu_);
         shards_.erase(key);
@@ -244,6 +313,20 @@ void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs
                 jobs.push_back(Job{i, key, p});
             }
         }
+        // A decoded (or failed) job: drop the pool once verified, else the
+        // reference's corruption error when every shard was pooled.
+        auto settle = [&](size_t j) {
+            const Job& jb = jobs[j];
+            const ReceiveEvent& e = (*evs)[jb.msg];
+            const Shard& msg = msgs[jb.msg].second;
+            if (e.verified) {
+                std::lock_guard<std::mutex> lk(mu_);
+                shards_.erase(jb.key);
+            } else if (jb.pool.size() == msg.TotalShards) {
+                (*sts)[jb.msg] = Status::Err(RS_ESINGULAR, "Could not put together the message due to corruption");
+            }
+        };
+        std::vector<size_t> verify_jobs;
         // Decode the phase's pools, grouped by (k, n, share length).
         std::map<std::tuple<uint64_t, uint64_t, size_t>, std::vector<size_t>> groups;
         for (size_t j = 0; j < jobs.size(); ++j) {
@@ -277,18 +360,24 @@ void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs
             for (size_t q = 0; q < ids.size(); ++q) {
                 const Job& jb = jobs[ids[q]];
                 ReceiveEvent& e = (*evs)[jb.msg];
-                const Shard& msg = msgs[jb.msg].second;
                 e.decode_status = st[q];
                 if (st[q].ok()) e.message = std::move(outs[q]);
-                e.verified = st[q].ok() && verify_ &&
-                             verify_(serializeMessage(msgs[jb.msg].first, e.message), msg.FileSignature);
-                if (e.verified) {
-                    std::lock_guard<std::mutex> lk(mu_);
-                    shards_.erase(jb.key);
-                } else if (jb.pool.size() == msg.TotalShards) {
-                    (*sts)[jb.msg] = Status::Err(RS_ESINGULAR,
-                                                 "Could not put together the message due to corruption");
-                }
+                if (st[q].ok() && verify_) verify_jobs.push_back(ids[q]);
+                else settle(ids[q]);
+            }
+        }
+        // Verify every decoded message of the phase: one GPU hash launch for
+        // all of them (hp.HashBytes of serializeMessage, main.go:82-89).
+        if (!verify_jobs.empty()) {
+            std::vector<std::vector<uint8_t>> ser, h;
+            ser.reserve(verify_jobs.size());
+            for (size_t j : verify_jobs) ser.push_back(serializeMessage(msgs[jobs[j].msg].first, (*evs)[jobs[j].msg].message));
+            const Status hs = HashBytes(ser, &h);
+            for (size_t v = 0; v < verify_jobs.size(); ++v) {
+                const size_t j = verify_jobs[v];
+                ReceiveEvent& e = (*evs)[jobs[j].msg];
+                e.verified = hs.ok() && verify_(h[v], msgs[jobs[j].msg].second.FileSignature);
+                settle(j);
             }
         }
         pending.swap(deferred);

@@ -9,9 +9,14 @@
 //   serializeMessage                                       main.go:276-302
 //   largestPrimeFactors (CLI k/n re-derivation)            main.go:303-335
 //   erasurecode.Shard + Marshal/Unmarshal/Size             protobuf/shard.proto:21-27
-// Networking, ed25519/blake2b signing and discovery are out of scope
-// (SURVEY.md §2): signing and verification are caller-supplied callbacks and
-// "broadcast" is a callback receiving each Shard.
+// Networking, ed25519 signing and discovery are out of scope:
+// the signature scheme is a caller-supplied callback and "broadcast" is a
+// callback receiving each Shard.  The hash policy (blake2b, main.go:38-41)
+// runs on the GPU when HashLen > 0: noise's Sign(sp, hp, msg) is
+// sp.Sign(hp.HashBytes(msg)), so the callbacks then receive the BLAKE2b
+// digest of serializeMessage(...) instead of the message itself, and
+// ReceiveBatch / prepareShardsBatch hash a whole batch in one launch
+// (rs_blake2b_batch).
 #pragma once
 
 #include <functional>
@@ -55,7 +60,8 @@ std::vector<uint8_t> serializeMessage(const PeerID& id, const std::vector<uint8_
 // main.go:303-335; -1 for n < 2 (the reference's initial value).
 int largestPrimeFactors(int n);
 
-// keys.Sign(policy, hash, msg) stand-in and crypto.Verify stand-in.
+// keys.Sign(policy, hash, msg) stand-in and crypto.Verify stand-in.  With
+// HashLen > 0 `msg` is blake2b-(8*HashLen)(serializeMessage(...)).
 using Signer = std::function<std::vector<uint8_t>(const std::vector<uint8_t>& msg)>;
 using Verifier = std::function<bool(const std::vector<uint8_t>& msg,
                                     const std::vector<uint8_t>& signature)>;
@@ -74,7 +80,11 @@ public:
     int MinimumNeededShards;
     int TotalShards;
 
-    ShardPlugin(int minimumNeededShards, int totalShards, Signer sign, Verifier verify);
+    // 0: sign/verify callbacks see the serialized message (no hash policy);
+    // 1..64: they see its BLAKE2b digest of that many bytes, hashed on the GPU.
+    int HashLen = 0;
+
+    ShardPlugin(int minimumNeededShards, int totalShards, Signer sign, Verifier verify, int hashLen = 0);
 
     // main.go:52-107.  `sender` = ctx.Sender().  The mempool update is done
     // under one lock (the reference's Load->Delete->Store on sync.Map is not
@@ -99,10 +109,19 @@ public:
     // main.go:211-241 (input == nullptr -> "network: input is null").
     Status prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
                          std::vector<Shard>* out);
+    // prepareShards for many inputs: every input's signature hash in one GPU
+    // launch (HashLen > 0), then shardInput per input.  (*out)[i] / (*sts)[i]
+    // correspond to inputs[i].
+    void prepareShardsBatch(const PeerID& self, const std::vector<std::vector<uint8_t>>& inputs,
+                            std::vector<std::vector<Shard>>* out, std::vector<Status>* sts);
     // main.go:243-267
     Status shardInput(const std::vector<uint8_t>& input, std::vector<Share>* out);
 
     size_t PoolSize(const std::vector<uint8_t>& fileSignature) const;
+
+    // hp.HashBytes over many messages (BLAKE2b, HashLen bytes, one GPU launch);
+    // with HashLen == 0 the messages are returned unchanged.
+    Status HashBytes(const std::vector<std::vector<uint8_t>>& msgs, std::vector<std::vector<uint8_t>>* out) const;
 
 private:
     Signer sign_;
@@ -111,9 +130,10 @@ private:
     std::unordered_map<std::string, std::vector<Share>> shards_;  // key: hex(signature)
 };
 
-// NewShardPlugin(signaturePolicy, hashPolicy, k, n)  main.go:108-115
+// NewShardPlugin(signaturePolicy, hashPolicy, k, n)  main.go:108-115;
+// hashLen > 0 selects the GPU BLAKE2b hash policy.
 std::unique_ptr<ShardPlugin> NewShardPlugin(Signer sign, Verifier verify, int minimumNeededShards,
-                                            int totalShards);
+                                            int totalShards, int hashLen = 0);
 
 std::string HexString(const std::vector<uint8_t>& b);  // fmt.Sprintf("%x", ...)
 

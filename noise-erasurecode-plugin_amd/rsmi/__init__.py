@@ -41,6 +41,7 @@ EXPORTS = (
     "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
     "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
+    "rs_blake2b_batch", "rs_blake2b_device",
 )
 
 
@@ -96,6 +97,8 @@ def _lib() -> ctypes.CDLL:
             "rs_device_free": (i32, [vp, vp]),
             "rs_stream_sync": (i32, [vp, vp]),
             "rs_fill_splitmix": (i32, [vp, vp, sz, ctypes.c_uint64, vp]),
+            "rs_blake2b_batch": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp]),
+            "rs_blake2b_device": (i32, [vp, i32, vp, vp, vp, i32, vp, vp]),
         }
         for name, (res, args) in sig.items():
             if os.environ.get("RSMI_LIB") and not hasattr(lib, name):
@@ -297,6 +300,32 @@ class FEC:
     def fill_splitmix(self, dev_ptr: int, nbytes: int, seed: int, stream: int = 0) -> None:
         _check(_lib().rs_fill_splitmix(self._h, dev_ptr, nbytes, seed & (2**64 - 1),
                                        stream or None), "rs_fill_splitmix")
+
+    # -- signature hashing (blake2b policy, main.go:38-41, :219-223, :82-89) ----
+    def blake2b_batch(self, messages: Sequence[bytes], digest_len: int = 32) -> List[bytes]:
+        """BLAKE2b digests of many host messages in one GPU launch."""
+        cnt = len(messages)
+        if cnt == 0:
+            return []
+        import numpy as np
+        lens_np = np.fromiter((len(mm) for mm in messages), dtype=np.uint64, count=cnt)
+        blob = b"".join(bytes(mm) for mm in messages)  # one buffer; pointers into it
+        base = ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p).value or 0
+        offs = np.zeros(cnt, dtype=np.uint64)
+        np.cumsum(lens_np[:-1], out=offs[1:])
+        ptr_np = (offs + np.uint64(base)).astype(np.uint64)
+        ptrs = ptr_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
+        lens = lens_np.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t))
+        out = ctypes.create_string_buffer(cnt * digest_len)
+        _check(_lib().rs_blake2b_batch(self._h, cnt, ptrs, lens, digest_len,
+                                       ctypes.cast(out, ctypes.c_void_p)), "rs_blake2b_batch")
+        raw = out.raw
+        return [raw[i * digest_len:(i + 1) * digest_len] for i in range(cnt)]
+
+    def blake2b_device(self, count: int, ptrs_dev: int, lens_dev: int, order_dev: int,
+                       digest_len: int, out_dev: int, stream: int = 0) -> None:
+        _check(_lib().rs_blake2b_device(self._h, count, ptrs_dev, lens_dev, order_dev or None,
+                                        digest_len, out_dev, stream or None), "rs_blake2b_device")
 
     def sync(self, stream: int = 0) -> None:
         _check(_lib().rs_stream_sync(self._h, stream or None), "rs_stream_sync")

@@ -292,3 +292,82 @@ def test_receive_batch_equals_sequential_receive():
         if b.verified:
             assert b.message == expect[m.FileSignature]
     assert sum(e.verified for e in bat_ev) == len(expect)
+
+
+# ------------------------------------------ hash policy on the GPU (§8f-4) ----
+def _digest_sign(seen):
+    """Signature stand-in over the digest the hash policy hands over
+    (noise: Sign(sp, hp, m) = sp.Sign(hp.HashBytes(m)))."""
+    def sign_d(d):
+        seen.append(bytes(d))
+        return hashlib.sha512(b"sig" + bytes(d)).digest()
+    return sign_d
+
+
+def _digest_verify(seen):
+    def verify_d(d, sig):
+        seen.append(bytes(d))
+        return hashlib.sha512(b"sig" + bytes(d)).digest() == sig
+    return verify_d
+
+
+@pytest.mark.parametrize("hash_len", [32, 64])
+def test_hash_policy_sign_and_verify_blake2b(hash_len):
+    """With the blake2b hash policy (main.go:38-41) the signer sees
+    blake2b(serializeMessage(self, input)) (main.go:219-223) and the verifier
+    blake2b(serializeMessage(sender, completeMessage)) (main.go:82-89),
+    computed on the GPU, bit-exact vs hashlib."""
+    k, n = 10, 14
+    signed, verified = [], []
+    p = h.NewShardPlugin(_digest_sign(signed), _digest_verify(verified), k, n, hash_len=hash_len)
+    blob = oracle.splitmix_bytes(1 << 20, 0x5EED).tobytes() + b"\0" * 4
+    shards = p.prepareShards(SELF, blob)
+    assert signed == [hashlib.blake2b(h.serializeMessage(SELF, blob), digest_size=hash_len).digest()]
+    recv = h.NewShardPlugin(_digest_sign([]), _digest_verify(verified), k, n, hash_len=hash_len)
+    ev = None
+    for i in (13, 1, 2, 3, 5, 7, 8, 9, 11, 12, 0):
+        ev = recv.Receive(SELF, shards[i])
+    assert ev.decoded and ev.verified and ev.message == blob
+    assert verified == [hashlib.blake2b(h.serializeMessage(SELF, blob), digest_size=hash_len).digest()]
+
+
+def test_hash_policy_receive_batch_hashes_in_one_pass():
+    """ReceiveBatch with the blake2b policy: every message decoded in a phase
+    is hashed in one GPU launch; all verify, digests equal hashlib's, and a
+    message whose shards were tampered with fails verification."""
+    k, n, L = 4, 6, 4000
+    verified = []
+    send = h.NewShardPlugin(_digest_sign([]), _digest_verify([]), k, n, hash_len=32)
+    recv = h.NewShardPlugin(_digest_sign([]), _digest_verify(verified), k, n, hash_len=32)
+    rng = np.random.default_rng(17)
+    blobs = [oracle.splitmix_bytes(L, 40 + i).tobytes() for i in range(24)]
+    all_shards = [send.prepareShards(SELF, b) for b in blobs]
+    bad = 5
+    tampered = all_shards[bad][2]
+    all_shards[bad][2] = h.Shard(tampered.FileSignature, bytes(len(tampered.ShardData)), 2, n, k)
+    arrivals = []
+    for shards in all_shards:
+        order = [int(x) for x in rng.permutation(n)][:k + 1]
+        if 2 not in order[:k]:
+            order = [2] + [i for i in order if i != 2][:k]
+        arrivals += [(SELF, shards[i]) for i in order]
+    evs, codes = recv.ReceiveBatch(arrivals)
+    done = [e for e in evs if e.decoded]
+    assert len(done) == len(blobs)
+    want = {hashlib.blake2b(h.serializeMessage(SELF, b), digest_size=32).digest() for b in blobs}
+    ok = [e for e in done if e.verified]
+    assert len(ok) == len(blobs) - 1
+    assert {e.message for e in ok} == set(blobs) - {blobs[bad]}
+    assert len(verified) == len(blobs) and set(verified) - want  # one digest is of the corrupted message
+    assert len(set(verified) & want) == len(blobs) - 1
+
+
+def test_prepare_shards_batch_matches_single():
+    k, n = 10, 14
+    p = h.NewShardPlugin(_digest_sign([]), _digest_verify([]), k, n, hash_len=32)
+    inputs = [oracle.splitmix_bytes(10 * (100 + 37 * i), 60 + i).tobytes() for i in range(40)] + [b"abc"]
+    out, codes = p.prepareShardsBatch(SELF, inputs)
+    assert codes[-1] != 0 and all(c == 0 for c in codes[:-1])  # len % k != 0 -> Encode error
+    for inp, shards in zip(inputs[:-1], out[:-1]):
+        assert shards == p.prepareShards(SELF, inp)
+    assert p.HashBytes([b"abc"]) == [hashlib.blake2b(b"abc", digest_size=32).digest()]
