@@ -272,13 +272,18 @@ def main():
         torch.distributed.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-
     enc_ms = [a.elapsed_time(b) for a, b, _ in ev]
     rec_ms = [b.elapsed_time(c) for _, b, c in ev]
+    # Per-rank wall time and kernel times; the job's time is the max.
+    mine = torch.tensor([elapsed, sum(enc_ms) / len(enc_ms), sum(rec_ms) / len(rec_ms)],
+                        dtype=torch.float64, device=dev)
+    if distributed:
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(gathered, mine)
+        per_rank = [g.tolist() for g in gathered]
+    else:
+        per_rank = [mine.tolist()]
+    elapsed = max(r[0] for r in per_rank)
     step_bytes_local = sum((enc_bytes if do_enc else 0) + (rec_bytes[i] if do_rec else 0)
                            for i in range(args.warmup, args.warmup + args.steps))
     total_bytes = step_bytes_local * world
@@ -300,6 +305,7 @@ def main():
     except (OSError, ValueError):
         pass
 
+    local_bytes = step_bytes_local
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
@@ -347,6 +353,10 @@ def main():
                 "algorithmic_bytes_per_launch": int(dom_bytes),
             },
             "cpu_baseline": cpu,
+            "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),
+                          "value": round(local_bytes / v[0] / 1e9, 2),
+                          "encode_ms": round(v[1], 3), "reconstruct_ms": round(v[2], 3)}
+                         for r, v in enumerate(per_rank)],
         }
         emit(out)
     if distributed:
@@ -357,8 +367,9 @@ def sharded_main(args, world, rank, local, dev, distributed):
     """configs[3], shard-distributed placement: shard i of every stripe is
     held by rank i mod N (the p2p analogue of main.go:207 broadcasting each
     shard to peers).  One step = the RCCL survivor gather (one grouped
-    send/recv, rsmi/distributed.py) + rs_reconstruct_stripes of the stripes
-    this rank owns.  Reported against the xGMI roofline (gathered bytes)."""
+    send/recv of exactly the survivors each owner reads, rsmi/distributed.py)
+    + rs_reconstruct_ptrs of the stripes this rank owns, reading survivors
+    where they landed.  Reported against the xGMI roofline (gathered bytes)."""
     import rsmi
     from rsmi import distributed as rd
 
@@ -367,7 +378,8 @@ def sharded_main(args, world, rank, local, dev, distributed):
     emax = args.emax if args.emax is not None else m
     gstripes = args.stripes * world          # global stripes; each rank owns args.stripes
     f = rsmi.FEC(k, n, device=local)
-    sh = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
     ids = rd.local_shard_ids(rank, n, world)
     held = torch.empty((gstripes, len(ids), S), dtype=torch.uint8, device=dev)
     # Setup (untimed): every rank encodes the global stripes in batches and
@@ -381,28 +393,39 @@ def sharded_main(args, world, rank, local, dev, distributed):
         f.encode_stripes(tmp_d.data_ptr(), k * S, tmp_p.data_ptr(), m * S, S, S, nb, sh)
         full = torch.cat([tmp_d[:nb * k * S].view(nb, k, S), tmp_p[:nb * m * S].view(nb, m, S)], 1)
         held[b0:b0 + nb] = full[:, ids, :]
+    del tmp_d, tmp_p
     if pattern_total(n, emax) <= (1 << 20):
         f.prepare_patterns(emax, sh)
-    torch.cuda.synchronize(dev)
     rng = np.random.default_rng(0xE4A5)  # same erasure map on every rank
     ersets = erasure_sets(rng, args.warmup + args.steps, gstripes, n, args.emin, emax,
                           args.pattern_pool)
     plans = [rd.plan_exchange(er, k, n, rank, world, S) for er in ersets]
+    bufs = rd.make_buffers(plans, S, dev)
+    tables = [torch.from_numpy(rd.shard_table(p, held, bufs)).to(dev) for p in plans]
+    torch.cuda.synchronize(dev)
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    def step(i):
-        out = rd.gather_survivors(held, plans[i], n)
-        owned = plans[i].owned
-        rd.reconstruct_owned(f, out, ersets[i][owned], sh)
-        return out
+    def step(i, timed):
+        e = gev[i - args.warmup] if timed else None
+        if e:
+            e[0].record(stream)
+        rd.gather_survivors(held, plans[i], bufs)
+        if e:
+            e[1].record(stream)
+        rd.reconstruct_owned(f, plans[i], tables[i], ersets[i][plans[i].owned], S, sh)
+        if e:
+            e[2].record(stream)
 
     for i in range(args.warmup):
-        step(i)
+        step(i, False)
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
-        step(i)
+        step(i, True)
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
@@ -410,13 +433,18 @@ def sharded_main(args, world, rank, local, dev, distributed):
     rec_bytes = sum(int(((k + ersets[i][plans[i].owned].sum(axis=1)) * S).sum())
                     for i in range(args.warmup, args.warmup + args.steps))
     xgmi_bytes = sum(plans[i].bytes_in for i in range(args.warmup, args.warmup + args.steps))
-    vals = torch.tensor([elapsed, rec_bytes, xgmi_bytes], dtype=torch.float64, device=dev)
+    g_ms = sum(a.elapsed_time(b) for a, b, _ in gev) / args.steps
+    r_ms = sum(b.elapsed_time(c) for _, b, c in gev) / args.steps
+    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, g_ms, r_ms], dtype=torch.float64, device=dev)
     if distributed:
-        mx = vals[:1].clone()
-        torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
-        torch.distributed.all_reduce(vals, op=torch.distributed.ReduceOp.SUM)
-        vals[0] = mx[0]
-    elapsed, rec_total, xgmi_total = (float(v) for v in vals.tolist())
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(gathered, mine)
+        per_rank = [g.tolist() for g in gathered]
+    else:
+        per_rank = [mine.tolist()]
+    elapsed = max(r[0] for r in per_rank)
+    rec_total = sum(r[1] for r in per_rank)
+    xgmi_total = sum(r[2] for r in per_rank)
     if rank == 0:
         xg = xgmi_total / elapsed / 1e9
         emit({
@@ -428,9 +456,14 @@ def sharded_main(args, world, rank, local, dev, distributed):
             "config": {"workload": f"RS({k},{n}) {args.emin}-{emax}-erasure reconstruct, shard i "
                                    f"on rank i mod N, {args.stripes} owned stripes x {S} B shards "
                                    "per rank", "placement": "sharded"},
-            "xgmi": {"gathered_GB": round(xgmi_total / 1e9, 3), "achieved_GBps_total": round(xg, 1),
-                     "per_rank_GBps": round(xg / max(world, 1), 1),
+            "xgmi": {"gathered_GB": round(xgmi_total / 1e9, 3), "gathered_GB_per_step": round(xgmi_total / args.steps / 1e9, 3),
+                     "achieved_GBps_total": round(xg, 1), "per_rank_GBps": round(xg / max(world, 1), 1),
                      "link_peak_GBps": 153.0, "links_per_gpu": 7},
+            "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),
+                          "gather_ms": round(v[3], 3), "reconstruct_ms": round(v[4], 3),
+                          "gathered_GB_per_step": round(v[2] / args.steps / 1e9, 3),
+                          "reconstruct_GBps": round(v[1] / v[0] / 1e9, 2)}
+                         for r, v in enumerate(per_rank)],
         })
     if distributed:
         torch.distributed.destroy_process_group()

@@ -140,6 +140,18 @@ int rs_reconstruct_stripes(rs_ctx *ctx, void *data, size_t data_stripe_stride,
                            size_t shard_len, size_t stripes, const uint8_t *erased,
                            void *stream);
 
+/* rs_reconstruct_ptrs: rs_reconstruct_stripes with shards anywhere in
+ * device memory.  shard_ptrs is a DEVICE array [stripes][n] of device
+ * addresses (16-byte aligned): shard i of stripe s is read (survivor) or
+ * written (erased) at shard_ptrs[s * n + i]; entries of present shards that
+ * Rebuild does not choose are never dereferenced.  shard_len bytes per
+ * shard (round_up(shard_len, 16) are coded).  The survivor gather of the
+ * shard-distributed placement reconstructs straight out of its receive
+ * buffers with it, and rs_decode_batch out of its packed
+ * staging.  Enqueued on stream. */
+int rs_reconstruct_ptrs(rs_ctx *ctx, const uint64_t *shard_ptrs, size_t shard_len, size_t stripes,
+                        const uint8_t *erased, void *stream);
+
 /* Cached decode patterns held by the ctx (diagnostics / tests).  The cache
  * holds at most 2^20 patterns (RSMI_PATTERN_CAP); a call that would exceed
  * that evicts it whole, with no host synchronisation (the rebuilt rows wait

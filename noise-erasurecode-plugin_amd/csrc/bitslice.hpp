@@ -54,6 +54,7 @@ struct BitsliceRecArgs {
     uint32_t ncols16;
     uint32_t blocks_per_stripe;
     const uint8_t* zpage;        // 2 KiB (one wave window) loaded for absent inputs
+    const uint64_t* shard_ptrs;  // [stripe][k + m] shard addresses (pointer mode), or nullptr
 };
 
 using BitsliceRecLaunch = hipError_t (*)(const BitsliceRecArgs&, hipStream_t);

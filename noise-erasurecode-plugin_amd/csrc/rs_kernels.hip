@@ -142,6 +142,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     }
 
     auto shard = [&](uint32_t id) -> uint8_t* {
+        if (a.shard_ptrs) return reinterpret_cast<uint8_t*>(a.shard_ptrs[s * (a.k + a.m) + id]);
         return id < a.k ? a.data + s * a.data_ss + static_cast<uint64_t>(id) * a.pitch
                         : a.parity + s * a.parity_ss + static_cast<uint64_t>(id - a.k) * a.pitch;
     };

@@ -36,6 +36,8 @@ struct MatArgs {
     const uint2* stripe_desc;    // [stripes] {stripe index, pattern id << 8 | outputs}
                                  // in processing order, or nullptr: stripe b, pattern 0
                                  // with all m rows (encode)
+    const uint64_t* shard_ptrs;  // [stripe][k + m] device address of every shard (pointer
+                                 // mode: data/parity/strides/pitch unused), or nullptr
 };
 
 // Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel

@@ -135,6 +135,25 @@ struct Staging {
 constexpr size_t kBatchChunks = 4;
 constexpr size_t kBatchChunkMin = size_t(16) << 20;
 
+// An erasure pattern as a 256-bit set of shard ids (n <= 256).
+struct PatKey {
+    uint64_t w[4];
+    bool operator==(const PatKey& o) const {
+        return w[0] == o.w[0] && w[1] == o.w[1] && w[2] == o.w[2] && w[3] == o.w[3];
+    }
+    bool has(int i) const { return (w[i >> 6] >> (i & 63)) & 1u; }
+};
+struct PatKeyHash {
+    size_t operator()(const PatKey& k) const {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (uint64_t v : k.w) {
+            h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+            h *= 0xBF58476D1CE4E5B9ull;
+        }
+        return static_cast<size_t>(h ^ (h >> 31));
+    }
+};
+
 namespace {
 
 // Per-call resources: every C-ABI call that needs a stream, staging or a
@@ -214,7 +233,7 @@ struct rs_ctx {
     // (each build first waits for the previous one), so a launch on any
     // stream that waits for it sees every row built so far.
     mutable std::shared_mutex pat_mu;
-    std::unordered_map<std::string, int> pat_index;
+    std::unordered_map<PatKey, int, PatKeyHash> pat_index;
     std::vector<uint32_t> h_src, h_dst, h_cnt;  // [npat][k], [npat][dst_stride], [npat]
     GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat;
     size_t uploaded = 0;    // patterns built on the device
@@ -387,24 +406,25 @@ bool pick_bitslice_rec(const rsmi::BitsliceKernel* b) {
 }
 
 // ----------------------------------------------------- pattern cache ----
-std::string pattern_key(const rs_ctx* c, const uint8_t* erased, int* count) {
-    std::string key(reinterpret_cast<const char*>(erased), static_cast<size_t>(c->n));
+PatKey pattern_key(const rs_ctx* c, const uint8_t* erased, int* count) {
+    PatKey key{{0, 0, 0, 0}};
     int e = 0;
-    for (char& ch : key) {
-        ch = ch ? 1 : 0;
-        e += ch;
-    }
+    for (int i = 0; i < c->n; ++i)
+        if (erased[i]) {
+            key.w[i >> 6] |= uint64_t(1) << (i & 63);
+            ++e;
+        }
     *count = e;
     return key;
 }
 
 // Creates the decode pattern for `key` (pat_mu held exclusively).
-int create_pattern(rs_ctx* c, std::string key) {
+int create_pattern(rs_ctx* c, const PatKey& key) {
     std::vector<uint8_t> present(c->n);
     std::vector<int> targets;
     for (int i = 0; i < c->n; ++i) {
-        present[i] = key[i] ? 0 : 1;
-        if (key[i]) targets.push_back(i);
+        present[i] = key.has(i) ? 0 : 1;
+        if (key.has(i)) targets.push_back(i);
     }
     std::vector<int> surv = rsmi::choose_survivors(present.data(), c->k, c->n);
     const int id = static_cast<int>(c->pat_index.size());
@@ -413,27 +433,31 @@ int create_pattern(rs_ctx* c, std::string key) {
     for (size_t t = 0; t < ds; ++t)
         c->h_dst.push_back(t < targets.size() ? static_cast<uint32_t>(targets[t]) : 0u);
     c->h_cnt.push_back(static_cast<uint32_t>(targets.size()));
-    c->pat_index.emplace(std::move(key), id);
+    c->pat_index.emplace(key, id);
     return id;
 }
 
+constexpr uint32_t kMissing = 0xFFFFFFFFu;
+
 // Pattern id of every stripe into pid.  With `create` (pat_mu exclusive)
 // missing patterns are added; without (pat_mu shared) they are counted in
-// *missing and their pid is left undefined.  More than m erasures in a
-// stripe -> RS_ENOT_ENOUGH.
+// *missing and their pid is kMissing.  With `only_missing`, stripes whose
+// pid is already set are skipped (the exclusive pass after a shared one).
+// More than m erasures in a stripe -> RS_ENOT_ENOUGH.
 int lookup_patterns(rs_ctx* c, const uint8_t* erased, size_t stripes, std::vector<uint32_t>& pid,
-                    bool create, size_t* missing) {
-    pid.resize(stripes);
+                    bool create, size_t* missing, bool only_missing = false) {
+    if (!only_missing) pid.assign(stripes, kMissing);
     size_t miss = 0;
     for (size_t i = 0; i < stripes; ++i) {
+        if (only_missing && pid[i] != kMissing) continue;
         int e = 0;
-        std::string key = pattern_key(c, erased + i * c->n, &e);
+        const PatKey key = pattern_key(c, erased + i * c->n, &e);
         if (e > c->m) return RS_ENOT_ENOUGH;
         auto it = c->pat_index.find(key);
         if (it != c->pat_index.end()) {
             pid[i] = static_cast<uint32_t>(it->second);
         } else if (create) {
-            pid[i] = static_cast<uint32_t>(create_pattern(c, std::move(key)));
+            pid[i] = static_cast<uint32_t>(create_pattern(c, key));
         } else {
             ++miss;
         }
@@ -538,7 +562,7 @@ void set_cache_patterns(const rs_ctx* c, rsmi::MatArgs& a) {
 // held, shared or exclusive, and every pattern built): stripe descriptors
 // through L's staging and device buffer, then one launch per kernel.
 int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_t pss, size_t pitch,
-                       size_t len, size_t stripes, hipStream_t s) {
+                       size_t len, size_t stripes, const uint64_t* shard_ptrs, hipStream_t s) {
     const std::vector<uint32_t>& pid = L.pid;
     int max_e = 0;
     for (size_t i = 0; i < stripes; ++i) max_e = std::max<int>(max_e, static_cast<int>(c->h_cnt[pid[i]]));
@@ -584,6 +608,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, n_lo);
         set_cache_patterns(c, a);
         a.stripe_desc = d_desc;
+        a.shard_ptrs = shard_ptrs;
         e = rsmi::launch_matmul(a, max_lo, s);
     }
     if (e == hipSuccess && used > n_lo) {
@@ -606,6 +631,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.ncols16 = a.ncols16;
         b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
         b.zpage = dev_zpage(c);
+        b.shard_ptrs = shard_ptrs;
         e = c->bitslice->reconstruct(b, s);
     }
     L.end(s);  // under pat_mu: an eviction waits for these launches
@@ -616,22 +642,30 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
 // a shared lock; only a call that meets new patterns takes it exclusively
 // (to create, build and, past the cap, evict).
 int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_t pss, size_t pitch,
-                size_t len, size_t stripes, const uint8_t* erased, hipStream_t s) {
+                size_t len, size_t stripes, const uint8_t* erased, const uint64_t* shard_ptrs, hipStream_t s) {
     size_t missing = 0;
+    uint64_t gen = 0;
     {
         std::shared_lock<std::shared_mutex> rl(c->pat_mu);
         const int rc = lookup_patterns(c, erased, stripes, L.pid, false, &missing);
         if (rc != RS_OK) return rc;
-        if (missing == 0) return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, s);
+        if (missing == 0) return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, shard_ptrs, s);
+        gen = c->evictions;
     }
     std::unique_lock<std::shared_mutex> wl(c->pat_mu);
-    if (c->pat_index.size() + missing > c->pat_cap) evict_patterns(c, s);
-    const int rc = lookup_patterns(c, erased, stripes, L.pid, true, nullptr);
+    // Only the stripes the shared pass missed are looked up again, unless
+    // the cache was evicted meanwhile (ids found then are stale).
+    bool stale = c->evictions != gen;
+    if (c->pat_index.size() + missing > c->pat_cap) {
+        evict_patterns(c, s);
+        stale = true;
+    }
+    const int rc = lookup_patterns(c, erased, stripes, L.pid, true, nullptr, !stale);
     if (rc != RS_OK) return rc;
     if (c->pat_index.size() > (size_t(1) << 24)) return RS_EINVAL;  // 24-bit ids in the descriptors
     const int st = flush_patterns(c, s);
     if (st != RS_OK) return st;
-    return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, s);
+    return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, shard_ptrs, s);
 }
 
 // out_t = decode row (surv -> targets[t]) applied to the survivors, on the
@@ -1043,7 +1077,21 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
     if (!lg.L) return RS_ENOMEM;
-    return reconstruct(c, *lg.L, data, dss, parity, pss, pitch, len, stripes, erased,
+    return reconstruct(c, *lg.L, data, dss, parity, pss, pitch, len, stripes, erased, nullptr,
+                       static_cast<hipStream_t>(stream));
+}
+
+int rs_reconstruct_ptrs(rs_ctx* c, const uint64_t* shard_ptrs, size_t len, size_t stripes, const uint8_t* erased,
+                        void* stream) {
+    if (!c || !erased || !shard_ptrs) return RS_EINVAL;
+    if (stripes == 0 || len == 0) return RS_OK;
+    if (round_up(len, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;  // 32-bit column offsets
+    if (reinterpret_cast<uintptr_t>(shard_ptrs) & 7u) return RS_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    return reconstruct(c, *lg.L, nullptr, 0, nullptr, 0, round_up(len, 16), len, stripes, erased, shard_ptrs,
                        static_cast<hipStream_t>(stream));
 }
 
@@ -1171,39 +1219,33 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
     }
     if (fast.empty()) return rc;
-    // 3. the rest: one reconstruct launch over a device [batch][n][pitch]
-    //    image.  PCIe carries only the k survivors of each message in (packed
-    //    [batch][k][pitch], scattered on the device) and only the regenerated
-    //    data shards out (gathered into [E][pitch]); present data shards go
-    //    from the caller's buffers to dst on the host.
-    const size_t pitch = round_up(S, 256), stripe = pitch * static_cast<size_t>(n);
+    // 3. the rest: one pointer-mode reconstruct launch.  PCIe carries only
+    //    the k survivors of each message in (packed [batch][k][pitch]) and
+    //    only the regenerated data shards out; the kernel reads survivors
+    //    where they landed and writes each erased shard to its own row of an
+    //    output buffer (data rows first), through a [batch][n] shard-address
+    //    table.  Present data shards go from the caller's buffers to dst on
+    //    the host.
+    const size_t pitch = round_up(S, 256);
     const size_t B = fast.size();
     std::vector<uint8_t> erased(B * static_cast<size_t>(n), 0);
-    std::vector<uint64_t> pin, pout;  // {src offset, dst offset} pairs
     std::vector<rsmi::CopyPool::Piece> in, direct;
-    std::vector<std::pair<size_t, uint8_t*>> regen;  // packed index -> dst
-    pin.reserve(2 * B * k);
-    for (size_t j = 0; j < B; ++j) {
-        size_t q = 0;
+    std::vector<uint8_t*> regen;  // output row r (< E) -> caller destination
+    size_t n_par_out = 0;
+    for (size_t j = 0; j < B; ++j)
         for (int i = 0; i < n; ++i) {
             const uint8_t* p = by[fast[j]][i];
-            if (!p) {
+            if (p) {
+                if (i < k) direct.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, p, S});
+            } else {
                 erased[j * n + i] = 1;
-                if (i < k) {
-                    pout.push_back(j * stripe + static_cast<size_t>(i) * pitch);
-                    pout.push_back(regen.size() * pitch);
-                    regen.push_back({regen.size(), dsts[fast[j]] + static_cast<size_t>(i) * S});
-                }
-                continue;
+                if (i < k) regen.push_back(dsts[fast[j]] + static_cast<size_t>(i) * S);
+                else ++n_par_out;
             }
-            const size_t slot = j * k + q++;  // exactly k present (fast path)
-            pin.push_back(slot * pitch);
-            pin.push_back(j * stripe + static_cast<size_t>(i) * pitch);
-            if (i < k) direct.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, p, S});
         }
-    }
     const size_t E = regen.size();
-    const size_t packed = std::max(B * static_cast<size_t>(k), E) * pitch;
+    const size_t packed = B * static_cast<size_t>(k) * pitch;
+    const size_t out_rows = E + n_par_out;
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1213,9 +1255,10 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     if (!pipe) return RS_ENOMEM;
     const hipStream_t s = L.stream;
     L.begin(s);  // the lease's buffers may last have been read on another stream
-    const size_t piece_bytes = (pin.size() + pout.size()) * sizeof(uint64_t);
-    if (!L.st_batch.acquire(packed) || !L.d_batch.reserve(B * stripe) || !L.d_pack.reserve(packed) ||
-        !L.st_pieces.acquire(piece_bytes) || !L.d_pieces.reserve(piece_bytes))
+    const size_t table_bytes = B * static_cast<size_t>(n) * sizeof(uint64_t);
+    if (!L.st_batch.acquire(std::max(packed, E * pitch)) || !L.d_pack.reserve(packed) ||
+        !L.d_batch.reserve(std::max<size_t>(out_rows, 1) * pitch) || !L.st_pieces.acquire(table_bytes) ||
+        !L.d_pieces.reserve(table_bytes))
         return RS_ENOMEM;
     // From the first async copy on, every exit waits for the stream: the
     // staging buffers may not be reused (or freed) while a DMA reads them.
@@ -1225,25 +1268,31 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         return code;
     };
     uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
+    uint8_t* dp = static_cast<uint8_t*>(L.d_pack.p);
+    uint8_t* dout = static_cast<uint8_t*>(L.d_batch.p);
+    uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
+    size_t r_data = 0, r_par = E;
     for (size_t j = 0; j < B; ++j) {
         size_t q = 0;
-        for (int i = 0; i < n; ++i)
-            if (const uint8_t* p = by[fast[j]][i]) in.push_back({h + (j * k + q++) * pitch, p, S});
+        for (int i = 0; i < n; ++i) {
+            uint64_t& t = tab[j * n + i];
+            if (const uint8_t* p = by[fast[j]][i]) {
+                const size_t slot = j * k + q++;  // exactly k present (fast path)
+                in.push_back({h + slot * pitch, p, S});
+                t = reinterpret_cast<uint64_t>(dp + slot * pitch);
+            } else {
+                t = reinterpret_cast<uint64_t>(dout + (i < k ? r_data++ : r_par++) * pitch);
+            }
+        }
     }
-    uint64_t* hp = static_cast<uint64_t*>(L.st_pieces.p);
-    std::copy(pin.begin(), pin.end(), hp);
-    std::copy(pout.begin(), pout.end(), hp + pin.size());
-    uint8_t* d = static_cast<uint8_t*>(L.d_batch.p);
-    uint8_t* dp = static_cast<uint8_t*>(L.d_pack.p);
-    const uint64_t* dpin = static_cast<const uint64_t*>(L.d_pieces.p);
-    const size_t sb = round_up(S, 16);
-    if (hipMemcpyAsync(L.d_pieces.p, hp, piece_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (hipMemcpyAsync(L.d_pieces.p, tab, table_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
         return finish(RS_EDEVICE);
+    L.st_pieces.release_after(s);
     // Survivors in, in chunks of messages: the host staging copy of chunk
     // i + 1 runs while chunk i crosses PCIe (the staging buffer is pinned,
     // so each hipMemcpyAsync returns at once).  `in` holds exactly k pieces
     // per message, in message order.
-    const size_t chunks = std::min<size_t>(B, B * k * pitch >= kBatchChunkMin ? kBatchChunks : 1);
+    const size_t chunks = std::min<size_t>(B, packed >= kBatchChunkMin ? kBatchChunks : 1);
     for (size_t ch = 0; ch < chunks; ++ch) {
         const size_t j0 = B * ch / chunks, j1 = B * (ch + 1) / chunks;
         pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
@@ -1251,20 +1300,20 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
             hipSuccess)
             return finish(RS_EDEVICE);
     }
-    if (rsmi::launch_copy_pieces(dp, d, dpin, static_cast<uint32_t>(pin.size() / 2), sb, s) != hipSuccess)
-        return finish(RS_EDEVICE);
-    const int st = reconstruct(c, L, d, stripe, d + pitch * k, stripe, pitch, S, B, erased.data(), s);
+    const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, pitch, S, B, erased.data(),
+                               static_cast<const uint64_t*>(L.d_pieces.p), s);
     if (st != RS_OK) return finish(st);
     // Regenerated data shards out, in chunks with an event each, so the host
     // copies chunk i into the callers' buffers while chunk i + 1 crosses.
+    // (The D2H reuses the survivor staging: the stream orders it after the
+    // H2D copies that read it.)
     const size_t ochunks = E == 0 ? 0 : std::min<size_t>(E, E * pitch >= kBatchChunkMin ? kBatchChunks : 1);
     int rc_dev = RS_OK;
-    if (E > 0 && rsmi::launch_copy_pieces(d, dp, dpin + pin.size(), static_cast<uint32_t>(E), sb, s) != hipSuccess)
-        rc_dev = RS_EDEVICE;
     size_t queued = 0;
     for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch, ++queued) {
         const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
-        if (hipMemcpyAsync(h + r0 * pitch, dp + r0 * pitch, (r1 - r0) * pitch, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        if (hipMemcpyAsync(h + r0 * pitch, dout + r0 * pitch, (r1 - r0) * pitch, hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
             hipEventRecord(L.ev[ch], s) != hipSuccess)
             rc_dev = RS_EDEVICE;
     }
@@ -1278,10 +1327,11 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         }
         std::vector<rsmi::CopyPool::Piece> out;
         out.reserve(r1 - r0);
-        for (size_t r = r0; r < r1; ++r) out.push_back({regen[r].second, h + regen[r].first * pitch, S});
+        for (size_t r = r0; r < r1; ++r) out.push_back({regen[r], h + r * pitch, S});
         pipe->copy(out);
     }
     const int fin = finish(rc_dev);
+    L.st_batch.release_after(s);
     return fin != RS_OK ? fin : rc;
 }
 

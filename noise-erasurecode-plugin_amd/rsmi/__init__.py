@@ -36,7 +36,8 @@ RS_ETOO_MANY_ERRORS = -16
 EXPORTS = (
     "rs_new", "rs_new_on_device", "rs_free", "rs_k", "rs_n", "rs_device",
     "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode", "rs_decode_batch",
-    "rs_encode_stripes", "rs_reconstruct_stripes", "rs_pattern_count", "rs_pattern_evictions",
+    "rs_encode_stripes", "rs_reconstruct_stripes", "rs_reconstruct_ptrs", "rs_pattern_count",
+    "rs_pattern_evictions",
     "rs_prepare_patterns",
     "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
@@ -87,6 +88,7 @@ def _lib() -> ctypes.CDLL:
                                       ctypes.POINTER(vp), sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
             "rs_encode_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp]),
             "rs_reconstruct_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp, vp]),
+            "rs_reconstruct_ptrs": (i32, [vp, vp, sz, sz, vp, vp]),
             "rs_pattern_count": (i32, [vp]),
             "rs_pattern_evictions": (ctypes.c_int64, [vp]),
             "rs_prepare_patterns": (i32, [vp, i32, vp]),
@@ -275,6 +277,17 @@ class FEC:
                                              parity_stride, pitch, shard_len, stripes,
                                              ctypes.cast(buf, ctypes.c_void_p), stream or None),
                "rs_reconstruct_stripes")
+
+    def reconstruct_ptrs(self, shard_ptrs_dev: int, shard_len: int, stripes: int, erased: bytes,
+                         stream: int = 0) -> None:
+        """rs_reconstruct_ptrs: shard i of stripe s at the device address in
+        the device array shard_ptrs_dev[s * n + i]."""
+        if len(erased) != stripes * self.n:
+            raise RSError(RS_EINVAL, "erased must hold stripes*n flags")
+        buf = ctypes.c_char_p(bytes(erased))
+        _check(_lib().rs_reconstruct_ptrs(self._h, shard_ptrs_dev, shard_len, stripes,
+                                          ctypes.cast(buf, ctypes.c_void_p), stream or None),
+               "rs_reconstruct_ptrs")
 
     def pattern_count(self) -> int:
         return _lib().rs_pattern_count(self._h)

@@ -11,9 +11,22 @@ Two placements:
   rule, the same rule the engine applies -- from their holders in ONE grouped
   point-to-point exchange (torch.distributed batch_isend_irecv = RCCL
   ncclGroupStart/ncclSend/ncclRecv/ncclGroupEnd over xGMI), then regenerates
-  the erased shards locally with rs_reconstruct_stripes.  Traffic per stripe
-  is the survivors not already on the owner (about k*S*(G-1)/G bytes), so
-  this variant is bound by xGMI, not HBM.
+  the erased shards with rs_reconstruct_ptrs.  Traffic per stripe is the
+  survivors not already on the owner (about k*S*(G-1)/G bytes), so this
+  variant is bound by xGMI, not HBM.
+
+Data path of one exchange (no unpack pass, no per-peer temporaries):
+  * sender: the rows a peer needs are packed once into that peer's
+    contiguous segment of one reusable send buffer (one gather per peer;
+    sending exactly the survivors moves n/k = 1.4x fewer xGMI bytes for
+    RS(10,4) than shipping whole holder slices);
+  * receiver: each peer's rows land by irecv in a contiguous segment of one
+    receive buffer, in the order the plan fixed;
+  * reconstruct: a [owned][n] table of device addresses points each survivor
+    at its row in the receive buffer (or the local holder buffer) and each
+    erased shard at a row of the output buffer; the engine reads and writes
+    through it (rs_reconstruct_ptrs), so nothing is copied into an owner
+    layout first.
 
 The exchange plan is a pure function of (n, k, G, erasure flags) and is
 computed identically on every rank; the erasure map is metadata every peer
@@ -21,10 +34,13 @@ knows (the plugin learns it from which Shard messages arrived).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Dict, List, Sequence, Tuple
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
+
+# Shard table entry kinds ([owned][n] per plan).
+LOCAL, REMOTE, OUTPUT, UNUSED = 0, 1, 2, 3
 
 
 def choose_survivors(erased_row: Sequence[int], k: int, n: int) -> List[int]:
@@ -64,20 +80,29 @@ def local_shard_ids(rank: int, n: int, world: int) -> List[int]:
 
 @dataclass
 class ExchangePlan:
-    """Row indices for one rank's part of the survivor gather.
+    """One rank's part of the survivor gather.
 
-    send[peer]: rows of this rank's holder buffer ([stripes * nloc, S] view)
-                to send to `peer`, in order.
-    recv[peer]: rows of this rank's owner buffer ([owned * n, S] view) that
-                the data received from `peer` lands in, in the same order.
-    local_src/local_dst: survivors this rank both holds and owns.
+    send[peer]:     rows of this rank's holder buffer ([stripes * nloc, S]
+                    view) that `peer` needs, in the order it expects them.
+    recv[peer]:     rows this rank receives from `peer`; they occupy rows
+                    [recv_off[peer], recv_off[peer] + recv[peer]) of the
+                    receive buffer.
+    kind/row:       [owned, n] where shard i of owned stripe j is: LOCAL
+                    (holder-buffer row), REMOTE (receive-buffer row), OUTPUT
+                    (erased: output-buffer row) or UNUSED (present but not
+                    read by Rebuild).
     """
     owned: List[int]
     send: Dict[int, np.ndarray]
-    recv: Dict[int, np.ndarray]
-    local_src: np.ndarray
-    local_dst: np.ndarray
+    recv: Dict[int, int]
+    recv_off: Dict[int, int]
+    kind: np.ndarray
+    row: np.ndarray
+    n_recv: int = 0
+    n_send: int = 0
+    n_out: int = 0
     bytes_in: int = 0
+    send_off: Dict[int, int] = field(default_factory=dict)
 
 
 def plan_exchange(erased: np.ndarray, k: int, n: int, rank: int, world: int,
@@ -85,74 +110,124 @@ def plan_exchange(erased: np.ndarray, k: int, n: int, rank: int, world: int,
     stripes = erased.shape[0]
     nloc = len(local_shard_ids(rank, n, world))
     owned = [s for s in range(stripes) if owner(s, world) == rank]
-    opos = {s: j for j, s in enumerate(owned)}
     send: Dict[int, List[int]] = {p: [] for p in range(world) if p != rank}
-    recv: Dict[int, List[int]] = {p: [] for p in range(world) if p != rank}
-    lsrc: List[int] = []
-    ldst: List[int] = []
+    recv_rows: Dict[int, List[tuple]] = {p: [] for p in range(world) if p != rank}
+    kind = np.full((len(owned), n), UNUSED, dtype=np.int8)
+    row = np.zeros((len(owned), n), dtype=np.int64)
+    n_out = 0
+    opos = {s: j for j, s in enumerate(owned)}
     for s in range(stripes):
         o = owner(s, world)
-        for i in choose_survivors(erased[s], k, n):
+        surv = choose_survivors(erased[s], k, n)
+        if o == rank:
+            j = opos[s]
+            for i in range(n):
+                if erased[s, i]:
+                    kind[j, i] = OUTPUT
+                    row[j, i] = n_out
+                    n_out += 1
+        for i in surv:
             hd = holder(i, world)
             if hd == rank and o == rank:
-                lsrc.append(s * nloc + i // world)
-                ldst.append(opos[s] * n + i)
+                kind[opos[s], i] = LOCAL
+                row[opos[s], i] = s * nloc + i // world
             elif hd == rank:
                 send[o].append(s * nloc + i // world)
             elif o == rank:
-                recv[hd].append(opos[s] * n + i)
-    as_arr = lambda d: {p: np.asarray(v, dtype=np.int64) for p, v in d.items()}
-    rb = sum(len(v) for v in recv.values()) * shard_bytes
-    return ExchangePlan(owned, as_arr(send), as_arr(recv), np.asarray(lsrc, dtype=np.int64),
-                        np.asarray(ldst, dtype=np.int64), rb)
+                recv_rows[hd].append((opos[s], i))
+    recv: Dict[int, int] = {}
+    recv_off: Dict[int, int] = {}
+    off = 0
+    for p in sorted(recv_rows):
+        recv_off[p] = off
+        for r, (j, i) in enumerate(recv_rows[p]):
+            kind[j, i] = REMOTE
+            row[j, i] = off + r
+        recv[p] = len(recv_rows[p])
+        off += recv[p]
+    send_off: Dict[int, int] = {}
+    soff = 0
+    for p in sorted(send):
+        send_off[p] = soff
+        soff += len(send[p])
+    return ExchangePlan(owned, {p: np.asarray(v, dtype=np.int64) for p, v in send.items()}, recv, recv_off,
+                        kind, row, n_recv=off, n_send=soff, n_out=n_out, bytes_in=off * shard_bytes,
+                        send_off=send_off)
 
 
-def gather_survivors(held, plan: ExchangePlan, n: int, group=None):
-    """Runs the exchange.  `held` is this rank's holder buffer, a
-    [stripes, nloc, S] uint8 tensor; returns the owner buffer [owned, n, S]
-    with every survivor of every owned stripe in place (other slots
-    undefined).  One batch_isend_irecv: RCCL groups it into a single
-    ncclGroupStart/End of point-to-point sends and receives."""
+@dataclass
+class GatherBuffers:
+    """Reusable per-rank buffers of the exchange (allocate once, pass to
+    every step): send [rows, S], receive [rows, S], output [rows, S]."""
+    send: object
+    recv: object
+    out: object
+
+
+def make_buffers(plans: Sequence[ExchangePlan], shard_bytes: int, device) -> GatherBuffers:
+    import torch
+    mk = lambda rows: torch.empty((max(rows, 1), shard_bytes), dtype=torch.uint8, device=device)
+    return GatherBuffers(mk(max(p.n_send for p in plans)), mk(max(p.n_recv for p in plans)),
+                         mk(max(p.n_out for p in plans)))
+
+
+def shard_table(plan: ExchangePlan, held, bufs: GatherBuffers) -> np.ndarray:
+    """[owned, n] int64 device addresses for rs_reconstruct_ptrs: every
+    survivor where it lies, every erased shard at its output row."""
+    S = held.shape[-1]
+    base = {LOCAL: held.data_ptr(), REMOTE: bufs.recv.data_ptr(), OUTPUT: bufs.out.data_ptr(),
+            UNUSED: held.data_ptr()}
+    t = np.empty(plan.kind.shape, dtype=np.int64)
+    for kd, b in base.items():
+        m = plan.kind == kd
+        t[m] = b + plan.row[m] * S if kd != UNUSED else b
+    return t
+
+
+def gather_survivors(held, plan: ExchangePlan, bufs: GatherBuffers, group=None):
+    """Runs the exchange: packs what each peer needs into its segment of
+    bufs.send, and receives every peer's rows into bufs.recv (contiguous
+    segments in plan.recv_off order).  `held` is this rank's holder buffer, a
+    [stripes, nloc, S] uint8 tensor.  One batch_isend_irecv: RCCL groups it
+    into a single ncclGroupStart/End of point-to-point sends and receives."""
     import torch
     import torch.distributed as dist
 
     stripes, nloc, S = held.shape
-    if (nloc == n and len(plan.owned) == stripes and not any(len(r) for r in plan.send.values())
-            and not any(len(r) for r in plan.recv.values())
-            and np.array_equal(plan.local_src, plan.local_dst)):
-        # One rank holds and owns everything in the owner layout already
-        # (N = 1): the survivors are in place, nothing moves.
-        return held
-    flat = held.reshape(stripes * nloc, S)
-    out = torch.empty((len(plan.owned), n, S), dtype=held.dtype, device=held.device)
-    oflat = out.view(len(plan.owned) * n, S)
+    flat = held.view(stripes * nloc, S)
     dev = held.device
     ops = []
-    recv_bufs = {}
-    for p, rows in plan.send.items():
+    for p, rows in sorted(plan.send.items()):
         if len(rows):
-            buf = flat.index_select(0, torch.from_numpy(rows).to(dev))
-            ops.append(dist.P2POp(dist.isend, buf, p, group))
-    for p, rows in plan.recv.items():
-        if len(rows):
-            recv_bufs[p] = torch.empty((len(rows), S), dtype=held.dtype, device=dev)
-            ops.append(dist.P2POp(dist.irecv, recv_bufs[p], p, group))
+            seg = bufs.send[plan.send_off[p]:plan.send_off[p] + len(rows)]
+            torch.index_select(flat, 0, torch.from_numpy(rows).to(dev, non_blocking=True), out=seg)
+            ops.append(dist.P2POp(dist.isend, seg, p, group))
+    for p, cnt in sorted(plan.recv.items()):
+        if cnt:
+            ops.append(dist.P2POp(dist.irecv, bufs.recv[plan.recv_off[p]:plan.recv_off[p] + cnt], p, group))
     reqs = dist.batch_isend_irecv(ops) if ops else []
-    if len(plan.local_src):
-        oflat.index_copy_(0, torch.from_numpy(plan.local_dst).to(dev),
-                          flat.index_select(0, torch.from_numpy(plan.local_src).to(dev)))
     for r in reqs:
         r.wait()
-    for p, buf in recv_bufs.items():
-        oflat.index_copy_(0, torch.from_numpy(plan.recv[p]).to(dev), buf)
-    return out
+    return bufs
 
 
-def reconstruct_owned(fec, owned_buf, erased_owned: np.ndarray, stream: int = 0) -> None:
-    """Regenerates the erased shards of the owner buffer [owned, n, S] in
-    place with the engine (data region = slots 0..k-1, parity = k..n-1)."""
-    stripes, n, S = owned_buf.shape
-    k = fec.k
-    base = owned_buf.data_ptr()
-    fec.reconstruct_stripes(base, n * S, base + k * S, n * S, S, S, stripes,
-                            np.ascontiguousarray(erased_owned, dtype=np.uint8).tobytes(), stream)
+def reconstruct_owned(fec, plan: ExchangePlan, table_dev, erased_owned: np.ndarray, shard_bytes: int,
+                      stream: int = 0) -> None:
+    """Regenerates the erased shards of the owned stripes into bufs.out
+    through the shard table (a device int64 tensor from shard_table)."""
+    fec.reconstruct_ptrs(table_dev.data_ptr(), shard_bytes, len(plan.owned),
+                         np.ascontiguousarray(erased_owned, dtype=np.uint8).tobytes(), stream)
+
+
+def shard_bytes_at(plan: ExchangePlan, held, bufs: GatherBuffers, j: int, i: int):
+    """The bytes of shard i of owned stripe j as the reconstruct sees them
+    (tests)."""
+    kd, r = int(plan.kind[j, i]), int(plan.row[j, i])
+    S = held.shape[-1]
+    if kd == LOCAL:
+        return held.reshape(-1, S)[r]
+    if kd == REMOTE:
+        return bufs.recv[r]
+    if kd == OUTPUT:
+        return bufs.out[r]
+    return None

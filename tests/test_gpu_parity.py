@@ -512,26 +512,78 @@ def test_config2_full_size_64GiB_roundtrip():
     torch.cuda.empty_cache()
 
 
-def test_distributed_owner_buffer_reconstruct_world1():
-    """rsmi.distributed with G = 1: the owner buffer [owned, n, S] layout
-    reconstructs in place through rs_reconstruct_stripes (the RCCL exchange
-    itself is covered by tests/test_distributed.py with gloo)."""
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_distributed_gather_and_pointer_reconstruct(world):
+    """rsmi.distributed end to end on one GPU: the holder buffers of `world`
+    ranks, each rank's plan, the sender-side packing into the send buffer
+    (what gather_survivors does before batch_isend_irecv), the transport
+    emulated by copying every send segment into the matching receive segment,
+    then rs_reconstruct_ptrs through each owner's shard table.  Outputs equal
+    the originals.  (The RCCL transport itself: tests/test_distributed.py
+    with gloo; world 1 calls gather_survivors, which moves nothing.)"""
     from rsmi import distributed as rd
-    k, n, S, stripes = 10, 14, 4096, 9
+    k, n, S, stripes = 10, 14, 4096, 19
     f = fec(k, n)
     data, parity = _dev_stripes(f, stripes, S, S, 31)
     f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), (n - k) * S, S, S, stripes)
     f.sync()
     full = torch.cat([data.view(stripes, k, S), parity.view(stripes, n - k, S)], dim=1).contiguous()
-    er = _erasures(np.random.default_rng(9), stripes, n, n - k)
-    plan = rd.plan_exchange(er, k, n, 0, 1, S)
-    held = full.clone()
-    out = rd.gather_survivors(held, plan, n)  # G = 1: every survivor is local
-    bad = torch.from_numpy(er.astype(bool)).cuda()
-    out[bad] = 0
-    rd.reconstruct_owned(f, out, er)
+    er = _erasures(np.random.default_rng(9 + world), stripes, n, n - k)
+    held = [full[:, rd.local_shard_ids(r, n, world), :].contiguous() for r in range(world)]
+    plans = [rd.plan_exchange(er, k, n, r, world, S) for r in range(world)]
+    bufs = [rd.make_buffers([plans[r]], S, "cuda") for r in range(world)]
+    if world == 1:
+        rd.gather_survivors(held[0], plans[0], bufs[0])
+    for p in range(world):  # sender packing, as gather_survivors does it
+        flat = held[p].view(-1, S)
+        for o, rows in plans[p].send.items():
+            if len(rows):
+                seg = bufs[p].send[plans[p].send_off[o]:plans[p].send_off[o] + len(rows)]
+                torch.index_select(flat, 0, torch.from_numpy(rows).cuda(), out=seg)
+    for o in range(world):  # the transport
+        for p, cnt in plans[o].recv.items():
+            if cnt:
+                so = plans[p].send_off[o]
+                bufs[o].recv[plans[o].recv_off[p]:plans[o].recv_off[p] + cnt].copy_(bufs[p].send[so:so + cnt])
+    for o in range(world):
+        pl = plans[o]
+        bufs[o].out.fill_(0xA5)
+        table = torch.from_numpy(rd.shard_table(pl, held[o], bufs[o])).cuda()
+        rd.reconstruct_owned(f, pl, table, er[pl.owned], S)
+        f.sync()
+        for j, s in enumerate(pl.owned):
+            for i in np.nonzero(er[s])[0]:
+                assert torch.equal(bufs[o].out[int(pl.row[j, i])], full[s, i]), (world, o, s, i)
+
+
+@pytest.mark.parametrize("k,n,S", [(10, 14, 4099), (64, 80, 8192), (4, 6, 100), (17, 49, 1000)])
+def test_reconstruct_ptrs_scattered_shards(k, n, S):
+    """rs_reconstruct_ptrs with every shard of every stripe at a random row of
+    one pool (random order, shards of different stripes interleaved) equals
+    the strided reconstruct: survivors read and erased shards written only
+    through the table, for the split-table and the bit-sliced (RS(64,16))
+    kernels."""
+    f = fec(k, n)
+    m = n - k
+    stripes = 24
+    pitch = (S + 15) // 16 * 16
+    data, parity = _dev_stripes(f, stripes, S, pitch, 600 + k)
+    f.encode_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes)
     f.sync()
-    assert torch.equal(out, full)
+    full = torch.cat([data.view(stripes, k, pitch), parity.view(stripes, m, pitch)], dim=1)
+    rng = np.random.default_rng(k * 3 + S)
+    er = _erasures(rng, stripes, n, m)
+    perm = rng.permutation(stripes * n)
+    pool = torch.empty((stripes * n, pitch), dtype=torch.uint8, device="cuda")
+    pool[torch.from_numpy(perm).cuda()] = full.reshape(stripes * n, pitch)
+    bad = torch.from_numpy(np.repeat(er.reshape(-1), 1).astype(bool))
+    pool[torch.from_numpy(perm[bad.numpy()]).cuda()] = 0x3C  # erased rows destroyed
+    table = torch.tensor((pool.data_ptr() + perm.astype(np.int64) * pitch).reshape(stripes, n),
+                         dtype=torch.int64, device="cuda")
+    f.reconstruct_ptrs(table.data_ptr(), S, stripes, er.tobytes())
+    f.sync()
+    got = pool[torch.from_numpy(perm).cuda()].view(stripes, n, pitch)
+    assert torch.equal(got[:, :, :S], full[:, :, :S])
 
 
 # ------------------------------------------------ GPU decode-row builder ----
