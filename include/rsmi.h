@@ -160,6 +160,16 @@ int rs_reconstruct_ptrs(rs_ctx *ctx, const uint64_t *shard_ptrs, size_t shard_le
 int rs_pattern_count(const rs_ctx *ctx);
 int64_t rs_pattern_evictions(const rs_ctx *ctx);
 
+/* Counters of a ctx (diagnostics / tests). */
+enum {
+    RS_STAT_PATTERNS = 0,          /* cached decode patterns                          */
+    RS_STAT_EVICTIONS = 1,         /* pattern-cache evictions                         */
+    RS_STAT_BATCHES_IN_PLACE = 2,  /* rs_decode_batch calls that read survivors in place */
+    RS_STAT_BATCHES_STAGED = 3,    /* ... that staged them through pinned copies      */
+    RS_STAT_LEASES = 4,            /* leases created (peak concurrent calls)          */
+};
+int64_t rs_stat(const rs_ctx *ctx, int which);
+
 /* Diagnostics: the decode rows the engine uses for one erasure pattern
  * (erased = n flags).  rows receives m*k bytes: row t (t < *count) is the
  * combination of the k survivors (Rebuild's choice) that regenerates the
@@ -196,9 +206,25 @@ int rs_blake2b_batch(rs_ctx *ctx, int count, const uint8_t *const *msgs, const s
 int rs_blake2b_device(rs_ctx *ctx, int count, const uint64_t *msg_ptrs, const uint64_t *lens,
                       const uint32_t *order, int digest_len, uint8_t *out, void *stream);
 
-/* ---- memory helpers ------------------------------------------------------ */
-void *rs_pinned_alloc(size_t bytes); /* hipHostMalloc; NULL on failure */
+/* ---- memory helpers ------------------------------------------------------
+ * Engine-pinned host memory (hipHostMalloc, mapped for the device).  The
+ * engine keeps a registry of these ranges: rs_decode_batch recognises
+ * survivors that lie in them (and are 16-byte aligned) without querying the
+ * runtime, and its reconstruct kernel reads them over PCIe in place -- no
+ * staging memcpy, no per-shard DMA (zero-copy receive, SURVEY.md §8f rank 1;
+ * the reference copies every ShardData at Unmarshal, shard.pb.go:468-503,
+ * and DeepCopy's every share, main.go:255-258). */
+void *rs_pinned_alloc(size_t bytes); /* NULL on failure */
 void rs_pinned_free(void *p);
+/* Receive arena: one pinned range carved into 256-byte aligned slots by a
+ * bump pointer (rs_shard_unmarshal_arena places ShardData in it).  Reset
+ * recycles every slot; not thread-safe (one arena per receiving thread). */
+typedef struct rs_arena rs_arena;
+rs_arena *rs_arena_new(size_t bytes);            /* NULL on failure */
+void *rs_arena_alloc(rs_arena *a, size_t bytes); /* NULL when full */
+void rs_arena_reset(rs_arena *a);
+size_t rs_arena_used(const rs_arena *a);
+void rs_arena_free(rs_arena *a);
 int rs_device_alloc(rs_ctx *ctx, size_t bytes, void **out);
 int rs_device_free(rs_ctx *ctx, void *p);
 int rs_stream_sync(rs_ctx *ctx, void *stream);

@@ -51,6 +51,14 @@ int rs_shard_marshal(const rs_shard_view *m, uint8_t *out, size_t cap, size_t *w
  * alias buf.  Absent fields are zero / empty. */
 int rs_shard_unmarshal(const uint8_t *buf, size_t len, rs_shard_view *out);
 
+struct rs_arena; /* rsmi.h */
+/* Unmarshal that places ShardData in a 16-byte aligned slot of `arena`
+ * (engine-pinned): the one copy gogo's Unmarshal makes anyway
+ * (shard.pb.go:468-503, `append(m.ShardData[:0], ...)`) lands where
+ * rs_decode_batch's kernel reads it in place.  FileSignature still aliases
+ * buf.  RS_ENOMEM (rsmi.h) when the arena is full. */
+int rs_shard_unmarshal_arena(const uint8_t *buf, size_t len, struct rs_arena *arena, rs_shard_view *out);
+
 #ifdef __cplusplus
 }
 #endif

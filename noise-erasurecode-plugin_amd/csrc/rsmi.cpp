@@ -26,6 +26,7 @@
 #include "gf256.hpp"
 #include "gf_invert.hpp"
 #include "host_pipeline.hpp"
+#include "pinned.hpp"
 #include "rs_kernels.hpp"
 
 namespace {
@@ -239,6 +240,7 @@ struct rs_ctx {
     size_t uploaded = 0;    // patterns built on the device
     size_t pat_cap = 0;     // soft bound; reaching it evicts the whole cache
     uint64_t evictions = 0;
+    std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
     hipEvent_t pat_ev = nullptr;
     bool pat_ev_valid = false;
     Staging st_pat;  // pattern-table uploads
@@ -993,6 +995,21 @@ int64_t rs_pattern_evictions(const rs_ctx* c) {
     return static_cast<int64_t>(c->evictions);
 }
 
+int64_t rs_stat(const rs_ctx* c, int which) {
+    if (!c) return RS_EINVAL;
+    switch (which) {
+        case RS_STAT_PATTERNS: return rs_pattern_count(c);
+        case RS_STAT_EVICTIONS: return rs_pattern_evictions(c);
+        case RS_STAT_BATCHES_IN_PLACE: return c->batches_in_place.load();
+        case RS_STAT_BATCHES_STAGED: return c->batches_staged.load();
+        case RS_STAT_LEASES: {
+            std::lock_guard<std::mutex> lk(const_cast<rs_ctx*>(c)->lease_mu);
+            return static_cast<int64_t>(c->leases.size());
+        }
+        default: return RS_EINVAL;
+    }
+}
+
 int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count) {
     if (!c || !erased || !rows || !count) return RS_EINVAL;
     DeviceGuard g(c->device);
@@ -1244,8 +1261,22 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
             }
         }
     const size_t E = regen.size();
-    const size_t packed = B * static_cast<size_t>(k) * pitch;
     const size_t out_rows = E + n_par_out;
+    // Zero-copy receive: when every survivor lies, 16-byte aligned, in
+    // engine-pinned memory (rs_pinned_alloc / rs_arena), the kernel reads it
+    // there over PCIe -- no staging copy, no H2D of survivors.
+    const size_t sb = round_up(S, 16);
+    std::vector<uint64_t> dev_of(B * static_cast<size_t>(n), 0);
+    bool in_place = std::getenv("RSMI_NO_DIRECT") == nullptr;
+    for (size_t j = 0; j < B && in_place; ++j)
+        for (int i = 0; i < n && in_place; ++i)
+            if (const uint8_t* p = by[fast[j]][i]) {
+                const uint64_t d = (reinterpret_cast<uintptr_t>(p) & 15u) ? 0 : rsmi::pinned_device_address(p, sb);
+                in_place = d != 0;
+                dev_of[j * n + i] = d;
+            }
+    const size_t packed = in_place ? 0 : B * static_cast<size_t>(k) * pitch;
+    ++(in_place ? c->batches_in_place : c->batches_staged);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1256,9 +1287,9 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     const hipStream_t s = L.stream;
     L.begin(s);  // the lease's buffers may last have been read on another stream
     const size_t table_bytes = B * static_cast<size_t>(n) * sizeof(uint64_t);
-    if (!L.st_batch.acquire(std::max(packed, E * pitch)) || !L.d_pack.reserve(packed) ||
-        !L.d_batch.reserve(std::max<size_t>(out_rows, 1) * pitch) || !L.st_pieces.acquire(table_bytes) ||
-        !L.d_pieces.reserve(table_bytes))
+    if (!L.st_batch.acquire(std::max<size_t>(std::max(packed, E * pitch), 16)) ||
+        (packed && !L.d_pack.reserve(packed)) || !L.d_batch.reserve(std::max<size_t>(out_rows, 1) * pitch) ||
+        !L.st_pieces.acquire(table_bytes) || !L.d_pieces.reserve(table_bytes))
         return RS_ENOMEM;
     // From the first async copy on, every exit waits for the stream: the
     // staging buffers may not be reused (or freed) while a DMA reads them.
@@ -1278,8 +1309,12 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
             uint64_t& t = tab[j * n + i];
             if (const uint8_t* p = by[fast[j]][i]) {
                 const size_t slot = j * k + q++;  // exactly k present (fast path)
-                in.push_back({h + slot * pitch, p, S});
-                t = reinterpret_cast<uint64_t>(dp + slot * pitch);
+                if (in_place) {
+                    t = dev_of[j * n + i];
+                } else {
+                    in.push_back({h + slot * pitch, p, S});
+                    t = reinterpret_cast<uint64_t>(dp + slot * pitch);
+                }
             } else {
                 t = reinterpret_cast<uint64_t>(dout + (i < k ? r_data++ : r_par++) * pitch);
             }
@@ -1288,11 +1323,11 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     if (hipMemcpyAsync(L.d_pieces.p, tab, table_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
         return finish(RS_EDEVICE);
     L.st_pieces.release_after(s);
-    // Survivors in, in chunks of messages: the host staging copy of chunk
-    // i + 1 runs while chunk i crosses PCIe (the staging buffer is pinned,
-    // so each hipMemcpyAsync returns at once).  `in` holds exactly k pieces
-    // per message, in message order.
-    const size_t chunks = std::min<size_t>(B, packed >= kBatchChunkMin ? kBatchChunks : 1);
+    // Staged survivors go in chunks of messages: the host staging copy of
+    // chunk i + 1 runs while chunk i crosses PCIe (the staging buffer is
+    // pinned, so each hipMemcpyAsync returns at once).  `in` holds exactly k
+    // pieces per message, in message order.
+    const size_t chunks = in_place ? 0 : std::min<size_t>(B, packed >= kBatchChunkMin ? kBatchChunks : 1);
     for (size_t ch = 0; ch < chunks; ++ch) {
         const size_t j0 = B * ch / chunks, j1 = B * (ch + 1) / chunks;
         pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
@@ -1431,16 +1466,6 @@ int rs_blake2b_batch(rs_ctx* c, int count, const uint8_t* const* msgs, const siz
     L.st_batch.release_after(s);
     L.st_pieces.release_after(s);
     return rc;
-}
-
-void* rs_pinned_alloc(size_t bytes) {
-    void* p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
-    return p;
-}
-
-void rs_pinned_free(void* p) {
-    if (p) (void)hipHostFree(p);
 }
 
 int rs_device_alloc(rs_ctx* c, size_t bytes, void** out) {

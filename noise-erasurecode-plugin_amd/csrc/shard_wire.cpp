@@ -6,6 +6,8 @@
 // MinimumNeededShards; empty bytes and zero integers are omitted.
 #include "../../include/rsmi_wire.h"
 
+#include "../../include/rsmi.h"
+
 #include <cstring>
 
 namespace {
@@ -186,6 +188,17 @@ int rs_shard_unmarshal(const uint8_t* buf, size_t len, rs_shard_view* out) {
             pos = pre + n;
         }
     }
+    return 0;
+}
+
+int rs_shard_unmarshal_arena(const uint8_t* buf, size_t len, rs_arena* arena, rs_shard_view* out) {
+    if (!arena) return RS_EINVAL;
+    const int rc = rs_shard_unmarshal(buf, len, out);
+    if (rc != 0 || out->shard_data_len == 0) return rc;
+    void* slot = rs_arena_alloc(arena, out->shard_data_len);
+    if (!slot) return RS_ENOMEM;
+    std::memcpy(slot, out->shard_data, out->shard_data_len);
+    out->shard_data = static_cast<const uint8_t*>(slot);
     return 0;
 }
 

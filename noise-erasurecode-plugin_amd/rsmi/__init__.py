@@ -43,6 +43,7 @@ EXPORTS = (
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
     "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
     "rs_blake2b_batch", "rs_blake2b_device",
+    "rs_stat", "rs_arena_new", "rs_arena_alloc", "rs_arena_reset", "rs_arena_used", "rs_arena_free",
 )
 
 
@@ -99,6 +100,13 @@ def _lib() -> ctypes.CDLL:
             "rs_device_free": (i32, [vp, vp]),
             "rs_stream_sync": (i32, [vp, vp]),
             "rs_fill_splitmix": (i32, [vp, vp, sz, ctypes.c_uint64, vp]),
+            "rs_stat": (ctypes.c_int64, [vp, i32]),
+            "rs_arena_new": (vp, [sz]),
+            "rs_arena_alloc": (vp, [vp, sz]),
+            "rs_arena_reset": (None, [vp]),
+            "rs_arena_used": (sz, [vp]),
+            "rs_arena_free": (None, [vp]),
+            "rs_shard_unmarshal_arena": (i32, [vp, sz, vp, vp]),
             "rs_blake2b_batch": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp]),
             "rs_blake2b_device": (i32, [vp, i32, vp, vp, vp, i32, vp, vp]),
         }
@@ -292,6 +300,11 @@ class FEC:
     def pattern_count(self) -> int:
         return _lib().rs_pattern_count(self._h)
 
+    STAT_PATTERNS, STAT_EVICTIONS, STAT_BATCHES_IN_PLACE, STAT_BATCHES_STAGED, STAT_LEASES = range(5)
+
+    def stat(self, which: int) -> int:
+        return _lib().rs_stat(self._h, which)
+
     def pattern_evictions(self) -> int:
         return _lib().rs_pattern_evictions(self._h)
 
@@ -342,6 +355,43 @@ class FEC:
 
     def sync(self, stream: int = 0) -> None:
         _check(_lib().rs_stream_sync(self._h, stream or None), "rs_stream_sync")
+
+
+class Arena:
+    """rs_arena: engine-pinned receive memory.  Shard bytes placed here (put,
+    or the wire codec's rs_shard_unmarshal_arena) are read in place over
+    PCIe by rs_decode_batch's kernel."""
+
+    def __init__(self, nbytes: int):
+        self._a = _lib().rs_arena_new(nbytes)
+        if not self._a:
+            raise RSError(RS_ENOMEM, "rs_arena_new")
+
+    def put(self, data: bytes) -> int:
+        """Copies data into a fresh 16-byte aligned slot; returns its address."""
+        p = _lib().rs_arena_alloc(self._a, len(data))
+        if not p:
+            raise RSError(RS_ENOMEM, "rs_arena_alloc")
+        if data:
+            ctypes.memmove(p, bytes(data), len(data))
+        return p
+
+    def used(self) -> int:
+        return _lib().rs_arena_used(self._a)
+
+    def reset(self) -> None:
+        _lib().rs_arena_reset(self._a)
+
+    def free(self) -> None:
+        if getattr(self, "_a", None):
+            _lib().rs_arena_free(self._a)
+            self._a = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def NewFEC(k: int, n: int) -> FEC:
