@@ -5,7 +5,7 @@
 // implemented over the MI355X engine's C ABI (include/rsmi.h) with cgo.
 //
 // The plugin changes only its import path; every call site compiles as is.
-// Requires Go >= 1.21 (runtime.Pinner) and lib/librsmi.so built by
+// Requires Go >= 1.21 (runtime.Pinner, min/max builtins) and lib/librsmi.so built by
 // `make -C noise-erasurecode-plugin_amd/csrc`.  Not compiled in this
 // repository's CI (no Go toolchain in the build image); see INTEGRATION.md.
 package infectious
@@ -15,6 +15,7 @@ package infectious
 #cgo LDFLAGS: -L${SRCDIR}/../../lib -lrsmi -Wl,-rpath,${SRCDIR}/../../lib
 #include <stdlib.h>
 #include "rsmi.h"
+#include "rsmi_wire.h"
 */
 import "C"
 
@@ -180,4 +181,156 @@ func (f *FEC) Decode(dst []byte, shares []Share) ([]byte, error) {
 		return nil, statusErr(st)
 	}
 	return dst, nil
+}
+
+// DecodeBatch decodes many messages of this code in one GPU pass
+// (rs_decode_batch; receive-side batching).  msgs[b] holds message b's
+// shares, all of one length.  It returns each message's output or error;
+// every message's shares are sorted in place like Decode sorts them.  When
+// every survivor lies in engine-pinned memory (an Arena filled by
+// UnmarshalShard), the GPU reads them there in place.
+func (f *FEC) DecodeBatch(msgs [][]Share) ([][]byte, []error) {
+	B := len(msgs)
+	outs := make([][]byte, B)
+	errs := make([]error, B)
+	if B == 0 {
+		return outs, errs
+	}
+	pieceLen := 0
+	total := 0
+	for _, m := range msgs {
+		if len(m) > 0 {
+			pieceLen = len(m[0].Data)
+		}
+		total += len(m)
+	}
+	for b, m := range msgs {
+		sort.Sort(byNumber(m))
+		for _, s := range m {
+			if len(s.Data) != pieceLen {
+				errs[b] = errors.New("infectious: shares have different lengths")
+			}
+		}
+		outs[b] = make([]byte, pieceLen*f.k)
+	}
+	for _, e := range errs {
+		if e != nil {
+			return outs, errs
+		}
+	}
+	cnt := max(total, 1)
+	counts := (*[1 << 28]C.int)(C.malloc(C.size_t(B) * C.size_t(unsafe.Sizeof(C.int(0)))))[:B:B]
+	nums := (*[1 << 28]C.int)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(C.int(0)))))[:cnt:cnt]
+	ptrs := (*[1 << 28]*C.uint8_t)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:cnt:cnt]
+	dsts := (*[1 << 28]*C.uint8_t)(C.malloc(C.size_t(B) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:B:B]
+	codes := (*[1 << 28]C.int)(C.malloc(C.size_t(B) * C.size_t(unsafe.Sizeof(C.int(0)))))[:B:B]
+	defer C.free(unsafe.Pointer(&counts[0]))
+	defer C.free(unsafe.Pointer(&nums[0]))
+	defer C.free(unsafe.Pointer(&ptrs[0]))
+	defer C.free(unsafe.Pointer(&dsts[0]))
+	defer C.free(unsafe.Pointer(&codes[0]))
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	j := 0
+	for b, m := range msgs {
+		counts[b] = C.int(len(m))
+		for i := range m {
+			nums[j] = C.int(m[i].Number)
+			ptrs[j] = nil
+			if pieceLen > 0 {
+				pinner.Pin(&m[i].Data[0])
+				ptrs[j] = (*C.uint8_t)(unsafe.Pointer(&m[i].Data[0]))
+			}
+			j++
+		}
+		dsts[b] = nil
+		if len(outs[b]) > 0 {
+			pinner.Pin(&outs[b][0])
+			dsts[b] = (*C.uint8_t)(unsafe.Pointer(&outs[b][0]))
+		}
+	}
+	C.rs_decode_batch(f.ctx, C.int(B), &counts[0], &nums[0], (**C.uint8_t)(unsafe.Pointer(&ptrs[0])),
+		C.size_t(pieceLen), (**C.uint8_t)(unsafe.Pointer(&dsts[0])), &codes[0])
+	for b := range msgs {
+		if codes[b] != C.RS_OK {
+			errs[b] = statusErr(codes[b])
+			outs[b] = nil
+		}
+	}
+	return outs, errs
+}
+
+// Arena is engine-pinned receive memory (rs_arena).  Shards unmarshalled
+// into it are read in place by the GPU.  Not safe for concurrent use: one
+// arena per receiving goroutine; Reset once its messages are decoded.
+type Arena struct{ a *C.rs_arena }
+
+// NewArena allocates an arena of the given size.
+func NewArena(bytes int) (*Arena, error) {
+	a := C.rs_arena_new(C.size_t(bytes))
+	if a == nil {
+		return nil, errors.New("infectious: pinned arena allocation failed")
+	}
+	return &Arena{a: a}, nil
+}
+
+// Reset recycles every slot of the arena.
+func (a *Arena) Reset() { C.rs_arena_reset(a.a) }
+
+// Free releases the arena's pinned memory.
+func (a *Arena) Free() { C.rs_arena_free(a.a); a.a = nil }
+
+// UnmarshalShard parses a wire erasurecode.Shard (protobuf/shard.proto:21-27)
+// and places ShardData in the arena -- the one copy gogo's Unmarshal makes
+// anyway (shard.pb.go:468-503).  The returned Share's Data aliases the arena
+// (valid until Reset); FileSignature is copied.
+func (a *Arena) UnmarshalShard(wire []byte) (sig []byte, s Share, total, need uint64, err error) {
+	var v C.rs_shard_view
+	var p *C.uint8_t
+	if len(wire) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(&wire[0]))
+	}
+	if st := C.rs_shard_unmarshal_arena(p, C.size_t(len(wire)), a.a, &v); st != 0 {
+		return nil, Share{}, 0, 0, fmt.Errorf("proto: Shard unmarshal failed (%d)", int(st))
+	}
+	sig = C.GoBytes(unsafe.Pointer(v.file_signature), C.int(v.file_signature_len))
+	s.Number = int(v.shard_number)
+	if v.shard_data_len > 0 {
+		s.Data = unsafe.Slice((*byte)(unsafe.Pointer(v.shard_data)), int(v.shard_data_len))
+	}
+	return sig, s, uint64(v.total_shards), uint64(v.minimum_needed_shards), nil
+}
+
+// HashBytes is the blake2b hash policy (main.go:38-41) for many messages in
+// one GPU launch (rs_blake2b_batch): digestLen bytes each (noise's policy:
+// 32).  Sign / Verify then run on the digests (main.go:219-223, :82-89).
+func (f *FEC) HashBytes(msgs [][]byte, digestLen int) ([][]byte, error) {
+	n := len(msgs)
+	if n == 0 {
+		return nil, nil
+	}
+	ptrs := (*[1 << 28]*C.uint8_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:n:n]
+	lens := (*[1 << 28]C.size_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.size_t(0)))))[:n:n]
+	defer C.free(unsafe.Pointer(&ptrs[0]))
+	defer C.free(unsafe.Pointer(&lens[0]))
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	for i, m := range msgs {
+		ptrs[i] = nil
+		lens[i] = C.size_t(len(m))
+		if len(m) > 0 {
+			pinner.Pin(&m[0])
+			ptrs[i] = (*C.uint8_t)(unsafe.Pointer(&m[0]))
+		}
+	}
+	out := make([]byte, n*digestLen)
+	if st := C.rs_blake2b_batch(f.ctx, C.int(n), (**C.uint8_t)(unsafe.Pointer(&ptrs[0])), &lens[0], C.int(digestLen),
+		(*C.uint8_t)(unsafe.Pointer(&out[0]))); st != C.RS_OK {
+		return nil, statusErr(st)
+	}
+	res := make([][]byte, n)
+	for i := range res {
+		res[i] = out[i*digestLen : (i+1)*digestLen]
+	}
+	return res, nil
 }

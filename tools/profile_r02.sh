@@ -1,0 +1,6 @@
+# r02 profiles: headline RS(10,4) (bench defaults) and BASELINE config 5
+# RS(64,16) 64 KiB shards (bit-sliced encode + bit-sliced syndrome reconstruct),
+# kernel trace + FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh).
+set -o pipefail
+PROF_TAG=r02 bash tools/profile.sh || exit 1
+PROF_TAG=r02_cfg5 PROF_ARGS="--k 64 --n 80 --shard 65536 --stripes 16384 --emax 16 --pattern-pool 256" bash tools/profile.sh || exit 1
