@@ -77,7 +77,9 @@ __device__ __forceinline__ void load_step(const uint4* src, uint32_t (&T)[kStepW
     }
 }
 
-// acc[r][w] ^= coef(row r) * x.w for the four rows of one sub-step.
+// acc[r][w] ^= coef(row r) * x.w for the first R rows of one sub-step (R < 4
+// only in the last sub-step of a row group that is not a multiple of 4).
+template <int R = kRowsPerStep>
 __device__ __forceinline__ void mac_step(uint32_t (&acc)[kRowsPerStep][4], const uint4& x,
                                          const uint32_t (&T)[kStepWords]) {
     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
@@ -87,7 +89,7 @@ __device__ __forceinline__ void mac_step(uint32_t (&acc)[kRowsPerStep][4], const
         const uint32_t ib = (xw[w] >> 3) & 0x07070707u;
         const uint32_t ic = (xw[w] >> 6) & 0x03030303u;
 #pragma unroll
-        for (int r = 0; r < kRowsPerStep; ++r) acc[r][w] = gf_mac(acc[r][w], &T[r * 5], ia, ib, ic);
+        for (int r = 0; r < R; ++r) acc[r][w] = gf_mac(acc[r][w], &T[r * 5], ia, ib, ic);
     }
 }
 
@@ -105,8 +107,9 @@ __device__ __forceinline__ void step_fence(uint32_t (&acc)[kRowsPerStep][4]) {
 // MG output rows.  LDS: [k][MG/4][20] table dwords | k survivor pointers.
 template <int K, int MG, int BT, bool NT>
 __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
-    static_assert(MG % kRowsPerStep == 0, "MG must be a multiple of 4");
-    constexpr int TG = MG / kRowsPerStep;                 // sub-steps per survivor
+    static_assert(MG % 2 == 0, "MG must be even");
+    constexpr int TG = (MG + kRowsPerStep - 1) / kRowsPerStep;  // sub-steps per survivor
+    constexpr int RL = MG - (TG - 1) * kRowsPerStep;            // rows in the last sub-step
     constexpr bool kRegPtrs = K > 0 && K <= 16;           // survivor bases kept in SGPRs
     constexpr int JB = (K == 0) ? 8 : (K <= 16 ? K : 8);  // survivor loads in flight
     const int k = K ? K : static_cast<int>(a.k);
@@ -174,9 +177,9 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     // Output pointers are only needed at store time.  Rows are padded to 16
     // ids, so whole 4-id groups load unconditionally (s_load_dwordx4); rows
     // past eg point at a valid shard and are never stored.
-    uint8_t* dp[MG];
+    uint8_t* dp[TG * 4];
 #pragma unroll
-    for (int g = 0; g < MG / 4; ++g) {
+    for (int g = 0; g < TG; ++g) {
         const uint4 ids = *reinterpret_cast<const uint4*>(dstid + 4 * g);
         const uint32_t idv[4] = {ids.x, ids.y, ids.z, ids.w};
 #pragma unroll
@@ -239,7 +242,10 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
                     const int step = (jb + q) * TG + g;
                     const bool more = (g + 1 < TG) || (q + 1 < JB && (K != 0 || jb + q + 1 < k));
                     if (more) load_step(lds4 + static_cast<size_t>(step + 1) * (kStepWords / 4), TB);
-                    if (TG == 1 || g < tg_used) mac_step(acc[g], x[q], TA);
+                    if (TG == 1 || g < tg_used) {
+                        if (g == TG - 1) mac_step<RL>(acc[g], x[q], TA);
+                        else mac_step(acc[g], x[q], TA);
+                    }
                     step_fence(acc[g]);
 #pragma unroll
                     for (int w = 0; w < kStepWords; ++w) TA[w] = TB[w];
@@ -298,7 +304,9 @@ struct Variant {
 const Variant kVariants[] = {
     RS_VARIANT(10, 4, 256),   // RS(10,4): BASELINE configs 1-4
     RS_VARIANT(4, 4, 256),    // RS(4,2): plugin default (main.go:34-35)
-    RS_VARIANT(8, 8, 256),    // infectious example RS(8,14)
+    RS_VARIANT(8, 4, 256),    // infectious example RS(8,14): reconstructs of <= 4 erasures
+    RS_VARIANT(8, 6, 256),    // ... its encode (6 rows: no padded rows' products)
+    RS_VARIANT(8, 8, 256),
     RS_VARIANT(64, 4, 256),   // RS(64,16) reconstructs of <= 4 erasures (fewer VGPRs, smaller tables)
     RS_VARIANT(64, 8, 256),   // ... and <= 8
     RS_VARIANT(64, 16, 256),  // RS(64,16): BASELINE config 5
@@ -332,7 +340,10 @@ const Variant& pick(int k, int rows) {
         if (v.K != 0 && v.K == k && rows <= v.MG) return v;
     for (const Variant& v : kVariants)
         if (v.K == 64 && k == 64 && v.MG == 16) return v;  // RS(64, m > 16): row groups of 16
-    return rows <= 4 ? kVariants[6] : kVariants[7];
+    const int want_mg = rows <= 4 ? 4 : 8;  // runtime-k fall-backs
+    for (const Variant& v : kVariants)
+        if (v.K == 0 && v.MG == want_mg) return v;
+    return kVariants[0];  // unreachable: both runtime-k variants are listed
 }
 
 }  // namespace
@@ -351,7 +362,7 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     a.iters = std::min<uint32_t>(iters_cap, total_it);
     a.chunks = (total_it + a.iters - 1) / a.iters;
     a.groups = static_cast<uint32_t>((max_e + v.MG - 1) / v.MG);
-    const size_t lds = static_cast<size_t>(a.k) * v.MG * 5 * 4 + a.k * sizeof(void*);
+    const size_t lds = static_cast<size_t>(a.k) * ((v.MG + 3) / 4) * kStepWords * 4 + a.k * sizeof(void*);
     const uint64_t blocks = a.stripes * a.chunks * a.groups;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
     hipLaunchKernelGGL(v.fn, dim3(static_cast<uint32_t>(blocks)), dim3(v.BT), lds, stream, a);

@@ -335,11 +335,18 @@ class FEC:
             return []
         import numpy as np
         lens_np = np.fromiter((len(mm) for mm in messages), dtype=np.uint64, count=cnt)
-        blob = b"".join(bytes(mm) for mm in messages)  # one buffer; pointers into it
-        base = ctypes.cast(ctypes.c_char_p(blob), ctypes.c_void_p).value or 0
-        offs = np.zeros(cnt, dtype=np.uint64)
-        np.cumsum(lens_np[:-1], out=offs[1:])
-        ptr_np = (offs + np.uint64(base)).astype(np.uint64)
+        if cnt <= 1024 or int(lens_np.sum()) > (64 << 20):
+            # few or large messages: point at each one (no Python-side copy)
+            keep = [bytes(mm) for mm in messages]
+            ptr_np = np.fromiter((ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value or 0 for b in keep),
+                                 dtype=np.uint64, count=cnt)
+        else:
+            # many small messages: one joined buffer, pointers into it
+            keep = b"".join(bytes(mm) for mm in messages)
+            base = ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p).value or 0
+            offs = np.zeros(cnt, dtype=np.uint64)
+            np.cumsum(lens_np[:-1], out=offs[1:])
+            ptr_np = (offs + np.uint64(base)).astype(np.uint64)
         ptrs = ptr_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
         lens = lens_np.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t))
         out = ctypes.create_string_buffer(cnt * digest_len)

@@ -758,3 +758,35 @@ def test_host_api_pinned_buffers(k, n, S):
     finally:
         for p in (pin_in, pin_par, pin_dst):
             lib.rs_pinned_free(p)
+
+
+@pytest.mark.parametrize("S,pitch", [(100, 112), (65536, 65536), (4099, 4112)])
+def test_rs8_14_row_group_of_six(S, pitch):
+    """RS(8,14) (infectious's example code) encodes with a 6-row group
+    (K8_MG6: the last 4-row sub-step codes 2 rows) and reconstructs <= 4
+    erasures with K8_MG4: parity vs the oracle, round trip vs the originals."""
+    k, n = 8, 14
+    m = n - k
+    f = fec(k, n)
+    assert f.kernel_name(0).startswith("K8_MG6")
+    stripes = 9
+    data, parity = _dev_stripes(f, stripes, S, pitch, 88 + S)
+    f.encode_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes)
+    f.sync()
+    hd = data.cpu().numpy().reshape(stripes, k, pitch)
+    hp = parity.cpu().numpy().reshape(stripes, m, pitch)
+    E = oracle.fec_matrix(k, n)
+    for s in range(stripes):
+        assert hp[s, :, :S].tobytes() == oracle.encode(E, k, n, hd[s, :, :S].tobytes()), s
+    d0, p0 = data.clone(), parity.clone()
+    for emax in (4, 6):  # K8_MG4 for <= 4 outputs, K8_MG6 beyond
+        er = _erasures(np.random.default_rng(S + emax), stripes, n, m, emin=1, emax=emax)
+        data.copy_(d0)
+        parity.copy_(p0)
+        data.view(stripes, k, pitch)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+        parity.view(stripes, m, pitch)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+        f.reconstruct_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes,
+                              er.tobytes())
+        f.sync()
+        assert torch.equal(data.view(stripes, k, pitch)[:, :, :S], d0.view(stripes, k, pitch)[:, :, :S])
+        assert torch.equal(parity.view(stripes, m, pitch)[:, :, :S], p0.view(stripes, m, pitch)[:, :, :S])
