@@ -179,6 +179,12 @@ def cpu_baseline(k, n, S, seconds, threads):
     }
 
 
+def stats_device(dev):
+    """Where the per-rank statistics are all-gathered: the GPU under RCCL,
+    host memory under the gloo rehearsal backend."""
+    return dev if os.environ.get("RSMI_BENCH_BACKEND", "nccl") == "nccl" else torch.device("cpu")
+
+
 # The one JSON line goes to the real stdout; everything else written to fd 1
 # (RCCL's init banner, library prints) is sent to stderr so a driver reading
 # stdout sees only that line.
@@ -200,11 +206,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RSMI_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a
+    # device round-robin; the driver's runs use RCCL, one rank per GPU).
+    backend = os.environ.get("RSMI_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     distributed = "RANK" in os.environ  # launched by torch.distributed.run (any N)
     if distributed:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     if args.placement == "sharded":
         return sharded_main(args, world, rank, local, dev, distributed)
@@ -276,7 +290,7 @@ def main():
     rec_ms = [b.elapsed_time(c) for _, b, c in ev]
     # Per-rank wall time and kernel times; the job's time is the max.
     mine = torch.tensor([elapsed, sum(enc_ms) / len(enc_ms), sum(rec_ms) / len(rec_ms)],
-                        dtype=torch.float64, device=dev)
+                        dtype=torch.float64, device=stats_device(dev))
     if distributed:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         torch.distributed.all_gather(gathered, mine)
@@ -435,7 +449,7 @@ def sharded_main(args, world, rank, local, dev, distributed):
     xgmi_bytes = sum(plans[i].bytes_in for i in range(args.warmup, args.warmup + args.steps))
     g_ms = sum(a.elapsed_time(b) for a, b, _ in gev) / args.steps
     r_ms = sum(b.elapsed_time(c) for _, b, c in gev) / args.steps
-    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, g_ms, r_ms], dtype=torch.float64, device=dev)
+    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, g_ms, r_ms], dtype=torch.float64, device=stats_device(dev))
     if distributed:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         torch.distributed.all_gather(gathered, mine)

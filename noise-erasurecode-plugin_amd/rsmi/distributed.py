@@ -196,18 +196,27 @@ def gather_survivors(held, plan: ExchangePlan, bufs: GatherBuffers, group=None):
     stripes, nloc, S = held.shape
     flat = held.view(stripes * nloc, S)
     dev = held.device
-    ops = []
+    # gloo (CPU tests, and the bench's one-GPU rehearsal of N ranks) moves
+    # host tensors only: device segments are staged through host copies.
+    staged = held.is_cuda and dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "gloo"
+    ops, landing = [], []
     for p, rows in sorted(plan.send.items()):
         if len(rows):
             seg = bufs.send[plan.send_off[p]:plan.send_off[p] + len(rows)]
             torch.index_select(flat, 0, torch.from_numpy(rows).to(dev, non_blocking=True), out=seg)
-            ops.append(dist.P2POp(dist.isend, seg, p, group))
+            ops.append(dist.P2POp(dist.isend, seg.cpu() if staged else seg, p, group))
     for p, cnt in sorted(plan.recv.items()):
         if cnt:
-            ops.append(dist.P2POp(dist.irecv, bufs.recv[plan.recv_off[p]:plan.recv_off[p] + cnt], p, group))
+            seg = bufs.recv[plan.recv_off[p]:plan.recv_off[p] + cnt]
+            tgt = torch.empty(seg.shape, dtype=seg.dtype) if staged else seg
+            if staged:
+                landing.append((seg, tgt))
+            ops.append(dist.P2POp(dist.irecv, tgt, p, group))
     reqs = dist.batch_isend_irecv(ops) if ops else []
     for r in reqs:
         r.wait()
+    for seg, tgt in landing:
+        seg.copy_(tgt)
     return bufs
 
 
