@@ -80,7 +80,11 @@ const char *rs_kernel_name(const rs_ctx *ctx, int which);
  * input: len bytes, len % k == 0 (else RS_ELEN_NOT_MULTIPLE), S = len / k.
  * Data shares 0..k-1 are views input[i*S, (i+1)*S) (systematic, exactly as
  * infectious emits them); parity shares k..n-1 are written to
- * parity[(i-k)*S, (i-k+1)*S).  len == 0 is allowed (empty shares). */
+ * parity[(i-k)*S, (i-k+1)*S).  len == 0 is allowed (empty shares).
+ * When input and parity are engine-pinned (rs_pinned_alloc / rs_arena),
+ * 16-byte aligned with S % 16 == 0, and the code uses the split-table
+ * kernel, the kernel reads and writes them in place over PCIe; rs_decode
+ * likewise hands exactly-k engine-pinned survivors to rs_decode_batch. */
 int rs_encode(rs_ctx *ctx, const uint8_t *input, size_t len, uint8_t *parity);
 
 /* rs_decode replaces (*FEC).Decode(dst, shares) at main.go:77: Correct, then
@@ -167,6 +171,7 @@ enum {
     RS_STAT_BATCHES_IN_PLACE = 2,  /* rs_decode_batch calls that read survivors in place */
     RS_STAT_BATCHES_STAGED = 3,    /* ... that staged them through pinned copies      */
     RS_STAT_LEASES = 4,            /* leases created (peak concurrent calls)          */
+    RS_STAT_ENCODES_IN_PLACE = 5,  /* rs_encode calls served from engine-pinned memory */
 };
 int64_t rs_stat(const rs_ctx *ctx, int which);
 

@@ -241,6 +241,7 @@ struct rs_ctx {
     size_t pat_cap = 0;     // soft bound; reaching it evicts the whole cache
     uint64_t evictions = 0;
     std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
+    std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
     hipEvent_t pat_ev = nullptr;
     bool pat_ev_valid = false;
     Staging st_pat;  // pattern-table uploads
@@ -710,6 +711,41 @@ int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vecto
     return RS_OK;
 }
 
+// rs_encode straight from / to engine-pinned memory (pinned.hpp): the
+// split-table kernel reads the data shards and writes the parity over PCIe
+// in place through a one-stripe shard table -- no staging copies, no DMA.
+// Returns false (nothing done) unless the code is served by the split-table
+// kernel and every shard is 16-byte aligned inside a registered range.
+bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t* parity, int* rc) {
+    const size_t k = c->k, m = c->m, n = c->n;
+    if (c->bitslice || (S & 15u) || (reinterpret_cast<uintptr_t>(input) & 15u) ||
+        (reinterpret_cast<uintptr_t>(parity) & 15u) || std::getenv("RSMI_NO_DIRECT"))
+        return false;
+    const uint64_t din = rsmi::pinned_device_address(input, k * S);
+    const uint64_t dout = rsmi::pinned_device_address(parity, m * S);
+    if (!din || !dout) return false;
+    const hipStream_t s = L.stream;
+    L.begin(s);
+    if (!L.st_pieces.acquire(n * sizeof(uint64_t)) || !L.d_pieces.reserve(n * sizeof(uint64_t))) {
+        *rc = RS_ENOMEM;
+        return true;
+    }
+    uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
+    for (size_t i = 0; i < n; ++i) tab[i] = i < k ? din + i * S : dout + (i - k) * S;
+    rsmi::MatArgs a = base_args(c, nullptr, 0, nullptr, 0, S, S, 1);
+    set_patterns(c, 1, c->d_encpat.p, a);
+    a.stripe_desc = nullptr;
+    a.shard_ptrs = static_cast<const uint64_t*>(L.d_pieces.p);
+    hipError_t e = hipMemcpyAsync(L.d_pieces.p, tab, n * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    L.st_pieces.release_after(s);
+    if (e == hipSuccess) e = rsmi::launch_matmul(a, c->m, s);
+    const hipError_t sy = hipStreamSynchronize(s);
+    L.end(s);
+    *rc = (e == hipSuccess && sy == hipSuccess) ? RS_OK : RS_EDEVICE;
+    ++c->encodes_in_place;
+    return true;
+}
+
 // Rebuild from the present shares: data shares copied, missing ones
 // regenerated from Rebuild's survivors.
 int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
@@ -1002,6 +1038,7 @@ int64_t rs_stat(const rs_ctx* c, int which) {
         case RS_STAT_EVICTIONS: return rs_pattern_evictions(c);
         case RS_STAT_BATCHES_IN_PLACE: return c->batches_in_place.load();
         case RS_STAT_BATCHES_STAGED: return c->batches_staged.load();
+        case RS_STAT_ENCODES_IN_PLACE: return c->encodes_in_place.load();
         case RS_STAT_LEASES: {
             std::lock_guard<std::mutex> lk(const_cast<rs_ctx*>(c)->lease_mu);
             return static_cast<int64_t>(c->leases.size());
@@ -1122,6 +1159,8 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
     if (!lg.L) return RS_ENOMEM;
+    int rc_in_place = RS_OK;
+    if (encode_in_place(c, *lg.L, input, S, parity, &rc_in_place)) return rc_in_place;
     rsmi::HostPipeline* pipe = lg.L->pipeline();
     if (!pipe) return RS_ENOMEM;
     std::vector<const uint8_t*> srcs(c->k);
@@ -1170,6 +1209,22 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (share_len == 0) return RS_OK;
     for (int i = 0; i < n; ++i)
         if (present[i] && !by_id[i]) return RS_EINVAL;
+    // (below ~16 KiB shards the batch path's fixed costs outweigh the staging
+    // it saves: 64 KiB messages decode in 0.074 vs 0.063 ms, profiles/r02m)
+    if (distinct == k && count == k && share_len >= (size_t(16) << 10) && !std::getenv("RSMI_NO_DIRECT")) {
+        // Survivors in engine-pinned memory: one in-place reconstruct launch
+        // (rs_decode_batch reads them over PCIe without staging).
+        bool pinned = true;
+        for (int i = 0; i < count && pinned; ++i)
+            pinned = !(reinterpret_cast<uintptr_t>(ptrs[i]) & 15u) &&
+                     rsmi::pinned_device_address(ptrs[i], round_up(share_len, 16)) != 0;
+        if (pinned) {
+            int cnt = count, st = RS_OK;
+            uint8_t* d1 = dst;
+            const int rc = rs_decode_batch(c, 1, &cnt, numbers, shares, share_len, &d1, &st);
+            return rc != RS_OK ? rc : st;
+        }
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);

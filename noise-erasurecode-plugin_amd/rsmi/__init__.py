@@ -300,7 +300,8 @@ class FEC:
     def pattern_count(self) -> int:
         return _lib().rs_pattern_count(self._h)
 
-    STAT_PATTERNS, STAT_EVICTIONS, STAT_BATCHES_IN_PLACE, STAT_BATCHES_STAGED, STAT_LEASES = range(5)
+    (STAT_PATTERNS, STAT_EVICTIONS, STAT_BATCHES_IN_PLACE, STAT_BATCHES_STAGED, STAT_LEASES,
+     STAT_ENCODES_IN_PLACE) = range(6)
 
     def stat(self, which: int) -> int:
         return _lib().rs_stat(self._h, which)

@@ -79,6 +79,31 @@ def main():
                "encode_GBps_pcie_inclusive": round(size * n / k / t_enc / 1e9, 2),
                "decode4_ms": round(t_dec * 1e3, 3),
                "decode4_GBps_pcie_inclusive": round(size * n / k / t_dec / 1e9, 2)}
+        # The same calls on engine-pinned buffers (16-byte shards): the
+        # kernel reads and writes them in place over PCIe.
+        Sp = S // 16 * 16
+        if Sp:
+            sp = Sp * k
+            pin_in, pin_par, pin_dst = (lib.rs_pinned_alloc(sp), lib.rs_pinned_alloc(m * Sp),
+                                        lib.rs_pinned_alloc(sp))
+            ctypes.memmove(pin_in, blob.ctypes.data, sp)
+            e0 = f.stat(f.STAT_ENCODES_IN_PLACE)
+            t_penc = timeit(lambda: lib.rs_encode(f.handle, pin_in, sp, pin_par), reps)
+            assert f.stat(f.STAT_ENCODES_IN_PLACE) > e0
+            pkeep = [pin_in + i * Sp if i < k else pin_par + (i - k) * Sp for i in keep]
+
+            def pdec():
+                nums = (ctypes.c_int * len(keep))(*keep)
+                ptrs = (ctypes.c_void_p * len(keep))(*pkeep)
+                assert lib.rs_decode(f.handle, nums, ptrs, len(keep), Sp, P(pin_dst)) == 0
+            t_pdec = timeit(pdec, reps)
+            assert ctypes.string_at(pin_dst, sp) == blob[:sp].tobytes()
+            for q in (pin_in, pin_par, pin_dst):
+                lib.rs_pinned_free(q)
+            rec.update({"pinned_encode_ms": round(t_penc * 1e3, 3),
+                        "pinned_encode_GBps_pcie_inclusive": round(sp * n / k / t_penc / 1e9, 2),
+                        "pinned_decode4_ms": round(t_pdec * 1e3, 3),
+                        "pinned_decode4_GBps_pcie_inclusive": round(sp * n / k / t_pdec / 1e9, 2)})
         if size <= (64 << 20):
             t_cpu = timeit(lambda: oracle.encode(E, k, n, blob.tobytes()), 3)
             rec["cpu_oracle_scalar_encode_ms"] = round(t_cpu * 1e3, 3)
