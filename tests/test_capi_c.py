@@ -1,7 +1,9 @@
 """The C ABI driven from C (tests/capi/abi_check.c), the way the cgo shim
 drives it: encode/decode of the config-1 blob vs the oracle, receive batching
 from an arena, BLAKE2b known answers, error classes, 8 concurrent threads.
-Built by __graft_entry__.build(); run on the GPU box."""
+Built by __graft_entry__.build(); run on the GPU box.  Also the host-only
+ThreadSanitizer / AddressSanitizer builds of the shared copy pool
+(tests/capi/copypool_stress.cpp), which run on the CPU."""
 import os
 import subprocess
 
@@ -9,7 +11,8 @@ import pytest
 
 from conftest import ROOT
 
-BIN = os.path.join(ROOT, "tests", "capi", "build", "abi_check")
+BUILD = os.path.join(ROOT, "tests", "capi", "build")
+BIN = os.path.join(BUILD, "abi_check")
 
 
 def test_abi_check_builds():
@@ -21,3 +24,14 @@ def test_abi_check_runs_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "abi_check: ok" in r.stdout
+
+
+@pytest.mark.parametrize("variant,iters", [("copypool_tsan", 3), ("copypool_asan", 20)])
+def test_copy_pool_concurrent_callers_under_sanitizer(variant, iters):
+    exe = os.path.join(BUILD, variant)
+    assert os.path.exists(exe), "run __graft_entry__.build() (make -C tests/capi)"
+    env = dict(os.environ, RSMI_COPY_THREADS="8")
+    r = subprocess.run([exe, str(iters), "8"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "copypool_stress: ok" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr, r.stderr
