@@ -1,0 +1,56 @@
+"""bench.py's host-side pieces on the CPU: the config-3 erasure generator,
+the pattern count that decides up-front preparation, the CPU description and
+the cpu_baseline leg structure (the oracle timed on a tiny sample).  The GPU
+line itself is produced by the driver on an MI355X."""
+import numpy as np
+import pytest
+
+import bench
+
+
+def test_erasure_sets_counts_and_determinism():
+    n, stripes = 14, 500
+    a = bench.erasure_sets(np.random.default_rng(0xE4A5), 3, stripes, n, 1, 4)
+    b = bench.erasure_sets(np.random.default_rng(0xE4A5), 3, stripes, n, 1, 4)
+    assert len(a) == 3
+    for x, y in zip(a, b):
+        assert x.shape == (stripes, n) and x.dtype == np.uint8
+        assert np.array_equal(x, y)
+        e = x.sum(axis=1)
+        assert e.min() >= 1 and e.max() <= 4
+        assert set(np.unique(e)) == {1, 2, 3, 4}  # uniform count: all occur at this size
+    assert not np.array_equal(a[0], a[1])  # a fresh erasure set per step
+
+
+def test_erasure_sets_pattern_pool():
+    sets = bench.erasure_sets(np.random.default_rng(1), 2, 1000, 80, 1, 16, pool=7)
+    for er in sets:
+        assert len({row.tobytes() for row in er}) <= 7
+        assert er.sum(axis=1).max() <= 16
+
+
+def test_pattern_total_decides_preparation():
+    assert bench.pattern_total(14, 4) == 14 + 91 + 364 + 1001 == 1470
+    assert bench.pattern_total(6, 2) == 6 + 15
+    assert bench.pattern_total(80, 16) > (1 << 20)  # config 5: patterns built on demand
+
+
+def test_host_cpu_info():
+    info = bench.host_cpu_info()
+    assert set(info) == {"model", "host_cpus", "usable_cpus", "cgroup_quota_cpus"}
+    assert 1 <= info["usable_cpus"] <= info["host_cpus"]
+
+
+def test_cpu_baseline_legs():
+    cpu = bench.cpu_baseline(4, 6, 4096, 0.2, 2)
+    assert cpu["kind"] == "port" and cpu["unit"] == "GB/s" and cpu["cores"] == 2
+    assert set(cpu["legs"]) == {"scalar_1t", "scalar_all", "avx2_1t", "avx2_all"}
+    assert cpu["value"] == cpu["legs"]["avx2_all"]["GBps"] > 0
+    assert all(leg["stripes"] > 0 for leg in cpu["legs"].values())
+
+
+@pytest.mark.parametrize("backend,want", [("nccl", "meta"), ("gloo", "cpu")])
+def test_stats_device(monkeypatch, backend, want):
+    import torch
+    monkeypatch.setenv("RSMI_BENCH_BACKEND", backend)
+    assert bench.stats_device(torch.device("meta")).type == want
