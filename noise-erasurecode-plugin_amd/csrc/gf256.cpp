@@ -88,23 +88,28 @@ std::vector<uint8_t> systematic_matrix(int k, int n) {
     return E;
 }
 
-std::vector<int> choose_survivors(const uint8_t* present, int k, int n) {
-    std::vector<int> out;
+int choose_survivors_into(const uint8_t* present, int k, int n, int* out) {
     int avail = 0;
     for (int i = 0; i < n; ++i) avail += present[i] ? 1 : 0;
-    if (avail < k) return out;
-    std::vector<uint8_t> used(n, 0);
+    if (avail < k) return 0;
+    uint8_t used[256] = {};
     int hi = n - 1;
     for (int i = 0; i < k; ++i) {
         if (present[i] && !used[i]) {
-            out.push_back(i);
+            out[i] = i;
             used[i] = 1;
             continue;
         }
         while (hi >= 0 && (!present[hi] || used[hi])) --hi;
-        out.push_back(hi);
+        out[i] = hi;
         used[hi] = 1;
     }
+    return k;
+}
+
+std::vector<int> choose_survivors(const uint8_t* present, int k, int n) {
+    std::vector<int> out(static_cast<size_t>(k));
+    out.resize(static_cast<size_t>(choose_survivors_into(present, k, n, out.data())));
     return out;
 }
 

@@ -42,6 +42,9 @@ bool invert(uint8_t* a, int k);
 // share.  present[n] flags; returns the k chosen shard ids in slot order, or
 // an empty vector when fewer than k are present.
 std::vector<int> choose_survivors(const uint8_t* present, int k, int n);
+// The same into out[k] (no allocation); returns k, or 0 when fewer than k
+// are present.  n <= 256.
+int choose_survivors_into(const uint8_t* present, int k, int n, int* out);
 
 // Decode rows for a set of survivors: for every shard id in `targets`, the
 // row d such that shard[target] = sum_c d[c] * shard[survivors[c]].

@@ -118,15 +118,60 @@ __global__ __launch_bounds__(kThreads) void invert_patterns_kernel(InvertArgs a)
     uint8_t* dl = pos + k;          // dm: erased data indices D (slot order)
     uint8_t* ds = dl + dm;          // dm: the parity survivor in each of those slots
     uint8_t* Et = ds + dm;          // m * k: encode rows of the targets
+    uint32_t* svl = reinterpret_cast<uint32_t*>(sm + ((Et + m * k - sm + 3) & ~3));  // k: survivor ids
+    uint32_t* tvl = svl + k;        // m: erased ids
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, nwaves = kThreads / 64;
     const uint32_t p = a.first + blockIdx.x;
     const uint32_t* sv = a.src + static_cast<size_t>(p) * k;
     const uint32_t* tv = a.dst + static_cast<size_t>(p) * a.dst_stride;
-    const int e = static_cast<int>(a.cnt[p]);
     uint8_t* out = a.coef + static_cast<size_t>(p) * m * k;
     if (tid == 0) a.status[p] = 0u;  // set to 1 below if the survivor matrix is singular
+    if (a.keys) {
+        // The pattern's rows from its key.  Erased ids ascending (wave 0,
+        // one ballot per 64 ids); survivors by Rebuild's rule (thread 0,
+        // the loop of gf256.cpp choose_survivors_into): slot i keeps shard i
+        // if present, else takes the highest present shard not yet used.
+        const uint64_t* kw = a.keys + static_cast<size_t>(blockIdx.x) * 4;
+        const int n = k + m;
+        if (wave == 0) {
+            int base = 0;
+            for (int c0 = 0; c0 < n; c0 += 64) {
+                const uint64_t valid = n - c0 >= 64 ? ~0ull : ((1ull << (n - c0)) - 1ull);
+                const uint64_t er = kw[c0 >> 6] & valid;
+                const int at = base + __builtin_popcountll(er & ((1ull << lane) - 1ull));
+                if (((er >> lane) & 1ull) && at < m) tvl[at] = static_cast<uint32_t>(c0 + lane);
+                base += __builtin_popcountll(er);
+            }
+            if (lane == 0) sh[3] = base;
+        }
+        if (tid == 0) {
+            uint64_t used[4] = {0, 0, 0, 0};
+            auto erased = [&](int j) { return (kw[j >> 6] >> (j & 63)) & 1ull; };
+            auto taken = [&](int j) { return (used[j >> 6] >> (j & 63)) & 1ull; };
+            int hi = n - 1;
+            for (int i = 0; i < k; ++i) {
+                int pick = i;
+                if (erased(i) || taken(i)) {
+                    while (hi >= 0 && (erased(hi) || taken(hi))) --hi;
+                    pick = hi < 0 ? 0 : hi;  // hi < 0 needs > m erasures: the host rejects those
+                }
+                svl[i] = static_cast<uint32_t>(pick);
+                used[pick >> 6] |= 1ull << (pick & 63);
+            }
+        }
+        __syncthreads();
+        const int e0 = sh[3];
+        uint32_t* gsv = a.src + static_cast<size_t>(p) * k;
+        uint32_t* gtv = a.dst + static_cast<size_t>(p) * a.dst_stride;
+        for (int i = tid; i < k; i += kThreads) gsv[i] = svl[i];
+        for (int t = tid; t < static_cast<int>(a.dst_stride); t += kThreads) gtv[t] = t < e0 && t < m ? tvl[t] : 0u;
+        if (tid == 0) a.cnt[p] = static_cast<uint32_t>(e0);
+        sv = svl;
+        tv = tvl;
+    }
+    const int e = a.keys ? sh[3] : static_cast<int>(a.cnt[p]);
 
     for (int i = tid; i < 512; i += kThreads) ex[i] = a.gf_exp[i];
     for (int i = tid; i < 256; i += kThreads) lg[i] = a.gf_log[i];
@@ -236,8 +281,9 @@ __global__ __launch_bounds__(kThreads) void invert_patterns_kernel(InvertArgs a)
 
 size_t invert_lds_bytes(int k, int m) {
     const size_t dm = static_cast<size_t>(k < m ? k : m);
-    return 16 + invert_work_bytes(k, m) + 512 + 256 + 3 * static_cast<size_t>(k) + 2 * dm +
-           static_cast<size_t>(m) * k;
+    const size_t bytes = 16 + invert_work_bytes(k, m) + 512 + 256 + 3 * static_cast<size_t>(k) + 2 * dm +
+                         static_cast<size_t>(m) * k;
+    return ((bytes + 3) & ~size_t(3)) + 4 * static_cast<size_t>(k + m);  // + survivor / erased ids
 }
 
 hipError_t launch_invert(const InvertArgs& a, uint32_t count, hipStream_t stream) {

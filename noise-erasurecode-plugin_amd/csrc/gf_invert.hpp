@@ -12,9 +12,14 @@ struct InvertArgs {
     const uint8_t* enc;      // [n][k] systematic matrix
     const uint8_t* gf_exp;   // [512] 2^i (i < 510)
     const uint8_t* gf_log;   // [256]
-    const uint32_t* src;     // [npat][k] survivor ids
-    const uint32_t* dst;     // [npat][dst_stride] erased ids
-    const uint32_t* cnt;     // [npat] erased count
+    // With keys: pattern first + i is the erasure bitmask keys[i][0..3] (bit
+    // j set <=> shard j erased); the kernel derives its survivor ids
+    // (Rebuild's choice), erased ids and count and writes them to src, dst
+    // and cnt.  Without keys the three are inputs.
+    const uint64_t* keys;    // [count][4] or nullptr
+    uint32_t* src;           // [npat][k] survivor ids
+    uint32_t* dst;           // [npat][dst_stride] erased ids (zero past the count)
+    uint32_t* cnt;           // [npat] erased count
     uint32_t dst_stride;
     uint8_t* coef;           // [npat][m][k] decode rows (output)
     uint32_t first;          // first pattern id to build

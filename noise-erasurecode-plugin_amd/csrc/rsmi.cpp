@@ -18,7 +18,6 @@
 #include <new>
 #include <shared_mutex>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "bitslice.hpp"
@@ -26,6 +25,7 @@
 #include "gf256.hpp"
 #include "gf_invert.hpp"
 #include "host_pipeline.hpp"
+#include "pattern_index.hpp"
 #include "pinned.hpp"
 #include "rs_kernels.hpp"
 
@@ -75,21 +75,30 @@ struct DevBuf {
 struct GrowBuf {
     void* p = nullptr;
     size_t cap = 0;
+    // Outgrown buffers.  Launches enqueued before a growth (on any lease's
+    // stream) may still read them, so they are kept until release() instead
+    // of a device-wide sync here; x4 growth keeps them under 1/3 of `cap`.
+    std::vector<void*> retired;
+    // Grows to hold `bytes`, keeping the first `used` bytes (copied on s,
+    // which the caller has ordered after their last writer).
     bool reserve_keep(size_t bytes, size_t used, hipStream_t s) {
         if (bytes <= cap) return true;
-        const size_t want = std::max({bytes, size_t(4096), 2 * cap});
+        const size_t want = std::max({bytes, size_t(4096), 4 * cap});
         void* np = nullptr;
         if (hipMalloc(&np, want) != hipSuccess) return false;
-        if (p) {
-            if (used) (void)hipMemcpyAsync(np, p, std::min(used, cap), hipMemcpyDeviceToDevice, s);
-            (void)hipDeviceSynchronize();  // older launches may still read p
-            (void)hipFree(p);
+        if (p && used &&
+            hipMemcpyAsync(np, p, std::min(used, cap), hipMemcpyDeviceToDevice, s) != hipSuccess) {
+            (void)hipFree(np);
+            return false;
         }
+        if (p) retired.push_back(p);
         p = np;
         cap = want;
         return true;
     }
     void release() {
+        for (void* r : retired) (void)hipFree(r);
+        retired.clear();
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -137,23 +146,7 @@ constexpr size_t kBatchChunks = 4;
 constexpr size_t kBatchChunkMin = size_t(16) << 20;
 
 // An erasure pattern as a 256-bit set of shard ids (n <= 256).
-struct PatKey {
-    uint64_t w[4];
-    bool operator==(const PatKey& o) const {
-        return w[0] == o.w[0] && w[1] == o.w[1] && w[2] == o.w[2] && w[3] == o.w[3];
-    }
-    bool has(int i) const { return (w[i >> 6] >> (i & 63)) & 1u; }
-};
-struct PatKeyHash {
-    size_t operator()(const PatKey& k) const {
-        uint64_t h = 0x9E3779B97F4A7C15ull;
-        for (uint64_t v : k.w) {
-            h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-            h *= 0xBF58476D1CE4E5B9ull;
-        }
-        return static_cast<size_t>(h ^ (h >> 31));
-    }
-};
+using rsmi::PatKey;
 
 namespace {
 
@@ -173,6 +166,7 @@ struct Lease {
     DevBuf d_stripe_pat, d_batch, d_pack, d_pieces, d_onepat;
     std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
     std::vector<uint32_t> pid, start;          // reconstruct scratch
+    std::vector<uint64_t> sort_a, sort_b;      // (bucket, stripe) radix-sort scratch
 
     bool init() {
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
@@ -234,9 +228,10 @@ struct rs_ctx {
     // (each build first waits for the previous one), so a launch on any
     // stream that waits for it sees every row built so far.
     mutable std::shared_mutex pat_mu;
-    std::unordered_map<PatKey, int, PatKeyHash> pat_index;
-    std::vector<uint32_t> h_src, h_dst, h_cnt;  // [npat][k], [npat][dst_stride], [npat]
-    GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat;
+    rsmi::PatIndex pat_index;
+    std::vector<uint32_t> h_cnt;  // [npat] erased count of each pattern
+    std::vector<PatKey> h_key;    // keys of the patterns created since the last flush
+    GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat, d_pkey;
     size_t uploaded = 0;    // patterns built on the device
     size_t pat_cap = 0;     // soft bound; reaching it evicts the whole cache
     uint64_t evictions = 0;
@@ -409,34 +404,16 @@ bool pick_bitslice_rec(const rsmi::BitsliceKernel* b) {
 }
 
 // ----------------------------------------------------- pattern cache ----
-PatKey pattern_key(const rs_ctx* c, const uint8_t* erased, int* count) {
-    PatKey key{{0, 0, 0, 0}};
-    int e = 0;
-    for (int i = 0; i < c->n; ++i)
-        if (erased[i]) {
-            key.w[i >> 6] |= uint64_t(1) << (i & 63);
-            ++e;
-        }
-    *count = e;
-    return key;
-}
-
-// Creates the decode pattern for `key` (pat_mu held exclusively).
-int create_pattern(rs_ctx* c, const PatKey& key) {
-    std::vector<uint8_t> present(c->n);
-    std::vector<int> targets;
-    for (int i = 0; i < c->n; ++i) {
-        present[i] = key.has(i) ? 0 : 1;
-        if (key.has(i)) targets.push_back(i);
-    }
-    std::vector<int> surv = rsmi::choose_survivors(present.data(), c->k, c->n);
-    const int id = static_cast<int>(c->pat_index.size());
-    for (int v : surv) c->h_src.push_back(static_cast<uint32_t>(v));
-    const size_t ds = dst_stride(c);
-    for (size_t t = 0; t < ds; ++t)
-        c->h_dst.push_back(t < targets.size() ? static_cast<uint32_t>(targets[t]) : 0u);
-    c->h_cnt.push_back(static_cast<uint32_t>(targets.size()));
-    c->pat_index.emplace(key, id);
+// Creates the decode pattern for `key` (pat_mu held exclusively): an id, its
+// erased count and a pending key.  The survivor and erased-id rows are
+// derived from the key on the GPU when the pattern is built
+// (invert_patterns_kernel), so a fresh pattern costs the host one index
+// insert and 32 bytes of upload.
+int create_pattern(rs_ctx* c, const PatKey& key, int e) {
+    const int id = static_cast<int>(c->h_cnt.size());
+    c->h_cnt.push_back(static_cast<uint32_t>(e));
+    c->h_key.push_back(key);
+    c->pat_index.insert(key, id);
     return id;
 }
 
@@ -454,13 +431,13 @@ int lookup_patterns(rs_ctx* c, const uint8_t* erased, size_t stripes, std::vecto
     for (size_t i = 0; i < stripes; ++i) {
         if (only_missing && pid[i] != kMissing) continue;
         int e = 0;
-        const PatKey key = pattern_key(c, erased + i * c->n, &e);
+        const PatKey key = rsmi::pattern_key(erased + i * c->n, c->n, &e);
         if (e > c->m) return RS_ENOT_ENOUGH;
-        auto it = c->pat_index.find(key);
-        if (it != c->pat_index.end()) {
-            pid[i] = static_cast<uint32_t>(it->second);
+        const int id = c->pat_index.find(key);
+        if (id >= 0) {
+            pid[i] = static_cast<uint32_t>(id);
         } else if (create) {
-            pid[i] = static_cast<uint32_t>(create_pattern(c, key));
+            pid[i] = static_cast<uint32_t>(create_pattern(c, key, e));
         } else {
             ++miss;
         }
@@ -479,8 +456,7 @@ void evict_patterns(rs_ctx* c, hipStream_t s) {
         for (const std::unique_ptr<Lease>& L : c->leases) L->begin(s);
     }
     c->pat_index.clear();
-    c->h_src.clear();
-    c->h_dst.clear();
+    c->h_key.clear();
     c->h_cnt.clear();
     c->uploaded = 0;
     ++c->evictions;
@@ -498,44 +474,36 @@ void wait_patterns(rs_ctx* c, hipStream_t s) {
     if (c->pat_ev_valid) (void)hipStreamWaitEvent(s, c->pat_ev, 0);
 }
 
-// Uploads the ids of patterns created since the last flush and builds their
-// decode rows on the GPU (one workgroup per pattern), on stream s after the
-// previous build (pat_mu exclusive).
+// Uploads the keys of the patterns created since the last flush and builds
+// them on the GPU (one workgroup per pattern: survivor and erased-id rows
+// from the key, then the decode rows), on stream s after the previous build
+// (pat_mu exclusive).
 int flush_patterns(rs_ctx* c, hipStream_t s) {
     const size_t npat = c->h_cnt.size(), first = c->uploaded;
     if (npat == first) return RS_OK;
     wait_patterns(c, s);  // the growth copies below read rows an earlier build wrote
     const size_t k = c->k, m = c->m, ds = dst_stride(c);
+    const size_t cnt = npat - first, b_key = cnt * sizeof(PatKey);
+    if (c->h_key.size() != cnt) return RS_EINVAL;  // internal invariant
     if (!c->d_pcoef.reserve_keep(npat * m * k, first * m * k, s) ||
         !c->d_psrc.reserve_keep(npat * k * 4, first * k * 4, s) ||
         !c->d_pdst.reserve_keep(npat * ds * 4, first * ds * 4, s) ||
         !c->d_pcnt.reserve_keep(npat * 4, first * 4, s) ||
-        !c->d_pstat.reserve_keep(npat * 4, first * 4, s))
+        !c->d_pstat.reserve_keep(npat * 4, first * 4, s) || !c->d_pkey.reserve_keep(b_key, 0, s))
         return RS_ENOMEM;
-    const size_t cnt = npat - first;
-    const size_t b_src = cnt * k * 4, b_dst = cnt * ds * 4, b_cnt = cnt * 4;
-    if (!c->st_pat.acquire(b_src + b_dst + b_cnt)) return RS_ENOMEM;
-    uint8_t* h = static_cast<uint8_t*>(c->st_pat.p);
-    std::memcpy(h, c->h_src.data() + first * k, b_src);
-    std::memcpy(h + b_src, c->h_dst.data() + first * ds, b_dst);
-    std::memcpy(h + b_src + b_dst, c->h_cnt.data() + first, b_cnt);
-    hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(c->d_psrc.p) + first * k * 4, h, b_src,
-                                  hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(static_cast<uint8_t*>(c->d_pdst.p) + first * ds * 4, h + b_src, b_dst,
-                           hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(static_cast<uint8_t*>(c->d_pcnt.p) + first * 4, h + b_src + b_dst, b_cnt,
-                           hipMemcpyHostToDevice, s);
+    if (!c->st_pat.acquire(b_key)) return RS_ENOMEM;
+    std::memcpy(c->st_pat.p, c->h_key.data(), b_key);
+    hipError_t e = hipMemcpyAsync(c->d_pkey.p, c->st_pat.p, b_key, hipMemcpyHostToDevice, s);
     c->st_pat.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
     rsmi::InvertArgs ia{};
     ia.enc = dev_enc(c);
     ia.gf_exp = dev_enc(c) + static_cast<size_t>(c->n) * c->k;
     ia.gf_log = ia.gf_exp + 512;
-    ia.src = static_cast<const uint32_t*>(c->d_psrc.p);
-    ia.dst = static_cast<const uint32_t*>(c->d_pdst.p);
-    ia.cnt = static_cast<const uint32_t*>(c->d_pcnt.p);
+    ia.keys = static_cast<const uint64_t*>(c->d_pkey.p);
+    ia.src = static_cast<uint32_t*>(c->d_psrc.p);
+    ia.dst = static_cast<uint32_t*>(c->d_pdst.p);
+    ia.cnt = static_cast<uint32_t*>(c->d_pcnt.p);
     ia.dst_stride = static_cast<uint32_t>(ds);
     ia.coef = static_cast<uint8_t*>(c->d_pcoef.p);
     ia.first = static_cast<uint32_t>(first);
@@ -551,6 +519,7 @@ int flush_patterns(rs_ctx* c, hipStream_t s) {
     if (hipEventRecord(c->pat_ev, s) != hipSuccess) return RS_EDEVICE;
     c->pat_ev_valid = true;
     c->uploaded = npat;
+    c->h_key.clear();
     return RS_OK;
 }
 
@@ -576,29 +545,58 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     // (profiles/r01e_ab_minrec.log: the syndrome kernel wins from e = 1).
     const int split_e = use_bitslice_rec(c) ? c->bitslice_rec_min_e : (c->m + 1);
     auto high = [&](uint32_t p) { return static_cast<int>(c->h_cnt[p]) >= split_e; };
-    // Counting sort of the stripes by (kernel, pattern): each launch lists its
+    // Sort of the stripes by (kernel, pattern): each launch lists its
     // stripes grouped by pattern (see rs_kernels.hpp stripe_desc).  The
     // RSMI_NO_SORT knob keeps address order within a kernel (A/B runs).
     static const bool no_sort = std::getenv("RSMI_NO_SORT") != nullptr;
     const size_t npat = no_sort ? 1 : c->h_cnt.size();
     const size_t nb = 2 * npat;
     auto bucket = [&](size_t i) -> size_t { return (high(pid[i]) ? npat : 0) + (no_sort ? 0 : pid[i]); };
-    std::vector<uint32_t>& start = L.start;
-    start.assign(nb + 1, 0);
     int max_lo = 0;
+    size_t used = 0, n_lo = 0;
     for (size_t i = 0; i < stripes; ++i) {
         const uint32_t p = pid[i];
         if (!c->h_cnt[p]) continue;  // stripes with nothing erased are skipped
-        ++start[bucket(i) + 1];
-        if (!high(p)) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
+        ++used;
+        if (!high(p)) {
+            ++n_lo;
+            max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
+        }
     }
-    for (size_t b = 0; b < nb; ++b) start[b + 1] += start[b];
-    const size_t used = start[nb], n_lo = start[npat];
     if (!L.st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
     uint2* desc = static_cast<uint2*>(L.st_stripe.p);
-    for (size_t i = 0; i < stripes; ++i) {
+    auto put = [&](size_t slot, size_t i) {
         const uint32_t p = pid[i];
-        if (c->h_cnt[p]) desc[start[bucket(i)]++] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
+        desc[slot] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
+    };
+    if (nb <= 4 * stripes + 4096) {
+        std::vector<uint32_t>& start = L.start;
+        start.assign(nb + 1, 0);
+        for (size_t i = 0; i < stripes; ++i)
+            if (c->h_cnt[pid[i]]) ++start[bucket(i) + 1];
+        for (size_t b = 0; b < nb; ++b) start[b + 1] += start[b];
+        for (size_t i = 0; i < stripes; ++i)
+            if (c->h_cnt[pid[i]]) put(start[bucket(i)]++, i);
+    } else {
+        // Many more patterns than stripes (fresh-pattern workloads): an LSD
+        // radix sort of (bucket, stripe) pairs, 8 bucket bits per pass, instead
+        // of a histogram over every cached pattern.  Stable, like the
+        // counting sort: stripes of one bucket stay in address order.
+        std::vector<uint64_t>& keys = L.sort_a;
+        std::vector<uint64_t>& tmp = L.sort_b;
+        keys.clear();
+        for (size_t i = 0; i < stripes; ++i)
+            if (c->h_cnt[pid[i]]) keys.push_back(static_cast<uint64_t>(bucket(i)) << 32 | i);
+        tmp.resize(keys.size());
+        const int bits = 64 - __builtin_clzll(static_cast<unsigned long long>(nb));
+        for (int shift = 32; shift < 32 + bits; shift += 8) {
+            size_t hist[257] = {};
+            for (uint64_t v : keys) ++hist[((v >> shift) & 255u) + 1];
+            for (int d = 0; d < 256; ++d) hist[d + 1] += hist[d];
+            for (uint64_t v : keys) tmp[hist[(v >> shift) & 255u]++] = v;
+            keys.swap(tmp);
+        }
+        for (size_t j = 0; j < keys.size(); ++j) put(j, static_cast<size_t>(keys[j] & 0xFFFFFFFFu));
     }
     L.begin(s);  // the descriptor buffer's previous readers
     wait_patterns(c, s);
@@ -996,7 +994,7 @@ void rs_free(rs_ctx* c) {
         c->free_leases.clear();
         c->st_pat.destroy();
         for (DevBuf* b : {&c->d_encpat, &c->d_gf}) b->release();
-        for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt, &c->d_pstat}) b->release();
+        for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt, &c->d_pstat, &c->d_pkey}) b->release();
         if (c->pat_ev) (void)hipEventDestroy(c->pat_ev);
     }
     delete c;

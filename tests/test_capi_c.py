@@ -35,3 +35,14 @@ def test_copy_pool_concurrent_callers_under_sanitizer(variant, iters):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "copypool_stress: ok" in r.stdout
     assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr, r.stderr
+
+
+def test_pattern_index_under_sanitizer():
+    """The pattern cache's host index (csrc/pattern_index.cpp): the 8-at-a-time
+    key builder against a byte loop for every n <= 256, and the open-addressing
+    index against std::unordered_map across rehashes and clears (ASan/UBSan)."""
+    exe = os.path.join(BUILD, "pattern_index_test")
+    assert os.path.exists(exe), "run __graft_entry__.build() (make -C tests/capi)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "pattern_index_test: ok" in r.stdout

@@ -132,7 +132,9 @@ def test_unmarshal_into_arena_then_decode_in_place():
 def test_host_api_in_place_encode_decode(k, n, S):
     """rs_encode with input and parity in engine-pinned memory runs the
     split-table kernel on them in place (no staging); rs_decode of k pinned
-    survivors goes through the in-place batch path.  Bit-exact vs oracle."""
+    survivors goes through the in-place batch path from 16 KiB shards up
+    (below that the staged pipeline is faster, rsmi.cpp rs_decode).  Bit-exact
+    vs oracle."""
     lib = rsmi.load()
     f = rsmi.FEC(k, n)
     m = n - k
@@ -149,7 +151,7 @@ def test_host_api_in_place_encode_decode(k, n, S):
         ptrs = (ctypes.c_void_p * k)(*[pin_in + i * S if i < k else pin_par + (i - k) * S for i in keep[::-1]])
         b0 = f.stat(f.STAT_BATCHES_IN_PLACE)
         assert lib.rs_decode(f.handle, nums, ptrs, k, S, pin_dst) == rsmi.RS_OK
-        assert f.stat(f.STAT_BATCHES_IN_PLACE) == b0 + 1
+        assert f.stat(f.STAT_BATCHES_IN_PLACE) == b0 + (1 if S >= (16 << 10) else 0)
         assert ctypes.string_at(pin_dst, k * S) == data
         assert list(nums) == sorted(keep)
         # pageable parity: staged pipeline, same bytes
