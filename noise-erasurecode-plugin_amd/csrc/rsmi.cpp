@@ -238,6 +238,7 @@ struct rs_ctx {
     std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
     std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
     hipEvent_t pat_ev = nullptr;
+    hipStream_t build_stream = nullptr;  // pattern builds (flush_patterns), off every caller's stream
     bool pat_ev_valid = false;
     Staging st_pat;  // pattern-table uploads
 
@@ -447,13 +448,12 @@ int lookup_patterns(rs_ctx* c, const uint8_t* erased, size_t stripes, std::vecto
 }
 
 // Drops every cached pattern (pat_mu exclusive) without a host sync: the
-// next build, enqueued on s, waits on the device for the last launch of
-// every lease -- all launches that read the tables recorded their lease's
+// build stream waits on the device for the last launch of every lease -- all launches that read the tables recorded their lease's
 // event while holding pat_mu -- before it overwrites rows.
-void evict_patterns(rs_ctx* c, hipStream_t s) {
+void evict_patterns(rs_ctx* c) {
     {
         std::lock_guard<std::mutex> lk(c->lease_mu);
-        for (const std::unique_ptr<Lease>& L : c->leases) L->begin(s);
+        for (const std::unique_ptr<Lease>& L : c->leases) L->begin(c->build_stream);
     }
     c->pat_index.clear();
     c->h_key.clear();
@@ -476,12 +476,14 @@ void wait_patterns(rs_ctx* c, hipStream_t s) {
 
 // Uploads the keys of the patterns created since the last flush and builds
 // them on the GPU (one workgroup per pattern: survivor and erased-id rows
-// from the key, then the decode rows), on stream s after the previous build
-// (pat_mu exclusive).
-int flush_patterns(rs_ctx* c, hipStream_t s) {
+// from the key, then the decode rows), pat_mu exclusive.  Builds run on the
+// context's build stream, in order (growth copies included), so a build can
+// overlap the kernels already queued on the callers' streams; readers wait
+// for pat_ev (wait_patterns).
+int flush_patterns(rs_ctx* c) {
     const size_t npat = c->h_cnt.size(), first = c->uploaded;
     if (npat == first) return RS_OK;
-    wait_patterns(c, s);  // the growth copies below read rows an earlier build wrote
+    const hipStream_t s = c->build_stream;
     const size_t k = c->k, m = c->m, ds = dst_stride(c);
     const size_t cnt = npat - first, b_key = cnt * sizeof(PatKey);
     if (c->h_key.size() != cnt) return RS_EINVAL;  // internal invariant
@@ -658,13 +660,13 @@ int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_
     // the cache was evicted meanwhile (ids found then are stale).
     bool stale = c->evictions != gen;
     if (c->pat_index.size() + missing > c->pat_cap) {
-        evict_patterns(c, s);
+        evict_patterns(c);
         stale = true;
     }
     const int rc = lookup_patterns(c, erased, stripes, L.pid, true, nullptr, !stale);
     if (rc != RS_OK) return rc;
     if (c->pat_index.size() > (size_t(1) << 24)) return RS_EINVAL;  // 24-bit ids in the descriptors
-    const int st = flush_patterns(c, s);
+    const int st = flush_patterns(c);
     if (st != RS_OK) return st;
     return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, shard_ptrs, s);
 }
@@ -948,6 +950,10 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         delete c;
         return RS_EDEVICE;
     }
+    if (hipStreamCreateWithFlags(&c->build_stream, hipStreamNonBlocking) != hipSuccess) {
+        rs_free(c);
+        return RS_EDEVICE;
+    }
     // Encode pattern: coef = bottom rows, src = 0..k-1, dst = k..n-1, cnt = m.
     std::vector<uint32_t> src(k), dst(c->m), cnt(1, static_cast<uint32_t>(c->m));
     for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
@@ -996,6 +1002,7 @@ void rs_free(rs_ctx* c) {
         for (DevBuf* b : {&c->d_encpat, &c->d_gf}) b->release();
         for (GrowBuf* b : {&c->d_pcoef, &c->d_psrc, &c->d_pdst, &c->d_pcnt, &c->d_pstat, &c->d_pkey}) b->release();
         if (c->pat_ev) (void)hipEventDestroy(c->pat_ev);
+        if (c->build_stream) (void)hipStreamDestroy(c->build_stream);
     }
     delete c;
 }
@@ -1054,10 +1061,10 @@ int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count)
     const hipStream_t s = lg.L->stream;
     std::unique_lock<std::shared_mutex> wl(c->pat_mu);
     std::vector<uint32_t> pid;
-    if (c->pat_index.size() + 1 > c->pat_cap) evict_patterns(c, s);
+    if (c->pat_index.size() + 1 > c->pat_cap) evict_patterns(c);
     int st = lookup_patterns(c, erased, 1, pid, true, nullptr);
     if (st != RS_OK) return st;
-    st = flush_patterns(c, s);
+    st = flush_patterns(c);
     if (st != RS_OK) return st;
     const size_t id = pid[0], mk = static_cast<size_t>(c->m) * c->k;
     wait_patterns(c, s);
@@ -1081,7 +1088,7 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
     if (!g.ok) return RS_EDEVICE;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     std::unique_lock<std::shared_mutex> wl(c->pat_mu);
-    if (c->pat_index.size() + static_cast<size_t>(total) > c->pat_cap) evict_patterns(c, s);
+    if (c->pat_index.size() + static_cast<size_t>(total) > c->pat_cap) evict_patterns(c);
     std::vector<uint8_t> er(c->n);
     std::vector<uint32_t> pid;
     std::vector<int> idx;
@@ -1100,7 +1107,7 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
             for (int j = i + 1; j < e; ++j) idx[j] = idx[j - 1] + 1;
         }
     }
-    const int st = flush_patterns(c, s);
+    const int st = flush_patterns(c);
     if (st != RS_OK) return st;
     return pattern_status(c, 0, c->h_cnt.size(), s);  // synchronises s
 }
