@@ -46,3 +46,14 @@ def test_pattern_index_under_sanitizer():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "pattern_index_test: ok" in r.stdout
+
+
+def test_shard_wire_fuzz_under_sanitizer():
+    """The Shard codec on peer input (tests/capi/wire_fuzz.cpp, ASan/UBSan):
+    round trips, mutated and random encodings from exact-size buffers --
+    no read past the input, views inside it, error codes negative."""
+    exe = os.path.join(BUILD, "wire_fuzz")
+    assert os.path.exists(exe), "run __graft_entry__.build() (make -C tests/capi)"
+    r = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "wire_fuzz: ok" in r.stdout
