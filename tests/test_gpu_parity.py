@@ -790,3 +790,34 @@ def test_rs8_14_row_group_of_six(S, pitch):
         f.sync()
         assert torch.equal(data.view(stripes, k, pitch)[:, :, :S], d0.view(stripes, k, pitch)[:, :, :S])
         assert torch.equal(parity.view(stripes, m, pitch)[:, :, :S], p0.view(stripes, m, pitch)[:, :, :S])
+
+
+@pytest.mark.parametrize("k,n", [(10, 14), (64, 80), (200, 256)])
+def test_erasure_flags_any_nonzero_byte(k, n):
+    """rs_reconstruct_stripes treats any non-zero flag byte as erased (the
+    pattern key is built 8 flags at a time, csrc/pattern_index.cpp): flags of
+    0x80 / 0xFF / 0x01 mixed give the same bytes and the same patterns as
+    flags of 1, on shards spanning every key word for n = 256."""
+    f = fec(k, n)
+    m = n - k
+    stripes, S = 12, 4096
+    data, parity = _dev_stripes(f, stripes, S, S, 900 + n)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    d0, p0 = data.clone(), parity.clone()
+    rng = np.random.default_rng(n)
+    er = np.zeros((stripes, n), dtype=np.uint8)
+    for s in range(stripes):
+        er[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 1
+    odd = er * rng.choice(np.array([0x01, 0x80, 0xFF, 0x10], dtype=np.uint8), size=er.shape)
+    dv, pv = data.view(stripes, k, S), parity.view(stripes, m, S)
+    for flags in (er, odd):
+        for s in range(stripes):  # wipe the erased shards
+            for i in np.nonzero(er[s])[0]:
+                (dv[s, i] if i < k else pv[s, i - k]).fill_(0x5A)
+        before = f.pattern_count()
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, flags.tobytes())
+        f.sync()
+        assert torch.equal(data, d0) and torch.equal(parity, p0)
+        if flags is odd:
+            assert f.pattern_count() == before  # same keys as the 0/1 flags
