@@ -821,3 +821,33 @@ def test_erasure_flags_any_nonzero_byte(k, n):
         assert torch.equal(data, d0) and torch.equal(parity, p0)
         if flags is odd:
             assert f.pattern_count() == before  # same keys as the 0/1 flags
+
+
+def test_pattern_tables_grow_across_calls():
+    """A fresh random pattern for every stripe, call after call: the pattern
+    tables grow x4 several times (outgrown buffers retired, no device sync)
+    and every call's output stays exact.  RS(64,16), 16,384 stripes of
+    256-byte shards, 13 calls -> ~213k patterns."""
+    f = rsmi.FEC(64, 80)
+    k, m, n = 64, 16, 80
+    stripes, S = 16384, 256
+    data, parity = _dev_stripes(f, stripes, S, S, 4242)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    d0, p0 = data.clone(), parity.clone()
+    rng = np.random.default_rng(77)
+    for call in range(13):
+        er = np.zeros((stripes, n), dtype=np.uint8)
+        e = rng.integers(1, m + 1, size=stripes)
+        for s in range(stripes):
+            er[s, rng.choice(n, size=int(e[s]), replace=False)] = 1
+        data.copy_(d0)
+        parity.copy_(p0)
+        mask = torch.from_numpy(er).to("cuda").bool()
+        data.view(stripes, k, S)[mask[:, :k]] = 0
+        parity.view(stripes, m, S)[mask[:, k:]] = 0
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+        f.sync()
+        assert torch.equal(data, d0) and torch.equal(parity, p0), call
+    assert f.pattern_count() > 150000 and f.pattern_evictions() == 0
+    f.close()
