@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this job may use (affinity and cgroup quota)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--stream", action="store_true",
+                    help="configs[1] second mode: the stripes stream from pinned host memory "
+                         "(H2D data, encode, D2H parity per chunk, two HIP streams); "
+                         "PCIe-inclusive, never the headline")
+    ap.add_argument("--stream-chunk", type=int, default=32, help="stripes per streamed chunk")
     return ap.parse_args()
 
 
@@ -222,6 +227,8 @@ def main():
     dev = torch.device("cuda", local)
     if args.placement == "sharded":
         return sharded_main(args, world, rank, local, dev, distributed)
+    if args.stream:
+        return stream_main(args, world, rank, local, dev, distributed)
 
     import rsmi
 
@@ -387,6 +394,82 @@ def main():
                          for r, v in enumerate(per_rank)],
         }
         emit(out)
+    if distributed:
+        torch.distributed.destroy_process_group()
+
+
+def stream_main(args, world, rank, local, dev, distributed):
+    """configs[1], second mode: the same 6,553 stripes, but the
+    data starts in pinned host memory and the parity ends there.  Chunks of
+    --stream-chunk stripes alternate between two HIP streams: H2D copy of the
+    chunk's data, rs_encode_stripes, D2H copy of its parity, so one chunk's
+    copies overlap the other's.  The host side is a two-slot pinned ring
+    (reused for every chunk: the bytes repeat, the PCIe and HBM work does
+    not).  value = (k+m) bytes per stripe over the wall time; the PCIe rates
+    are reported beside it."""
+    import rsmi
+
+    k, n, S = args.k, args.n, args.shard
+    m = n - k
+    stripes, C = args.stripes, max(1, min(args.stream_chunk, args.stripes))
+    f = rsmi.FEC(k, n, device=local)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    h_data = [torch.empty(C * k * S, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    h_par = [torch.empty(C * m * S, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    d_data = [torch.empty(C * k * S, dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_par = [torch.empty(C * m * S, dtype=torch.uint8, device=dev) for _ in range(2)]
+    for slot in range(2):
+        f.fill_splitmix(d_data[slot].data_ptr(), d_data[slot].numel(), 0x5EED + slot, streams[slot].cuda_stream)
+        streams[slot].synchronize()
+        h_data[slot].copy_(d_data[slot].cpu())
+    chunks = [(s0, min(C, stripes - s0)) for s0 in range(0, stripes, C)]
+
+    def one_pass():
+        for i, (s0, nb) in enumerate(chunks):
+            slot = i & 1
+            st = streams[slot]
+            with torch.cuda.stream(st):
+                d_data[slot][:nb * k * S].copy_(h_data[slot][:nb * k * S], non_blocking=True)
+                f.encode_stripes(d_data[slot].data_ptr(), k * S, d_par[slot].data_ptr(), m * S, S, S, nb,
+                                 st.cuda_stream)
+                h_par[slot][:nb * m * S].copy_(d_par[slot][:nb * m * S], non_blocking=True)
+
+    for _ in range(args.warmup):
+        one_pass()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_pass()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    mine = torch.tensor([elapsed], dtype=torch.float64, device=stats_device(dev))
+    if distributed:
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(gathered, mine)
+        per_rank = [g.item() for g in gathered]
+    else:
+        per_rank = [elapsed]
+    elapsed = max(per_rank)
+    total = args.steps * stripes * world
+    if rank == 0:
+        emit({
+            "metric": "RS(10,4) encode GB/s streamed from pinned host memory (configs[1] second mode, PCIe-inclusive)",
+            "value": round(total * (k + m) * S / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes in a two-slot pinned host ring)",
+            "config": {"workload": f"RS({k},{n}) encode of {stripes} stripes x {k} x {S} B shards per GPU, "
+                                   f"data H2D and parity D2H in chunks of {C} stripes on two HIP streams",
+                       "k": k, "n": n, "shard_bytes": S, "stripes_per_gpu": stripes, "chunk_stripes": C},
+            "pcie": {"h2d_GBps": round(total * k * S / elapsed / 1e9, 2),
+                     "d2h_GBps": round(total * m * S / elapsed / 1e9, 2)},
+            "per_rank": [{"rank": r, "ms_per_step": round(v / args.steps * 1e3, 3)} for r, v in enumerate(per_rank)],
+        })
     if distributed:
         torch.distributed.destroy_process_group()
 
