@@ -2,6 +2,8 @@
 the pattern count that decides up-front preparation, the CPU description and
 the cpu_baseline leg structure (the oracle timed on a tiny sample).  The GPU
 line itself is produced by the driver on an MI355X."""
+import sys
+
 import numpy as np
 import pytest
 
@@ -54,3 +56,14 @@ def test_stats_device(monkeypatch, backend, want):
     import torch
     monkeypatch.setenv("RSMI_BENCH_BACKEND", backend)
     assert bench.stats_device(torch.device("meta")).type == want
+
+
+def test_parse_stream_mode(monkeypatch):
+    """bench.py --stream (configs[1] second mode) parses with its chunk size;
+    the default run stays device-resident."""
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert not a.stream and a.placement == "local"
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--stream", "--stream-chunk", "16"])
+    a = bench.parse()
+    assert a.stream and a.stream_chunk == 16
