@@ -15,6 +15,7 @@
 #include "rs_kernels.hpp"
 
 #include "gf_device.hpp"
+#include "xcd.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -117,7 +118,8 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     uint32_t* tw = reinterpret_cast<uint32_t*>(lds4);
     uint8_t** sptr = reinterpret_cast<uint8_t**>(tw + k * MG * 5);
 
-    uint64_t b = blockIdx.x;
+    // A stripe's chunks x row groups run on one XCD, in order (xcd.hpp).
+    uint64_t b = a.xcd ? xcd_block(blockIdx.x, a.chunks * a.groups, static_cast<uint32_t>(a.stripes)) : blockIdx.x;
     const uint32_t grp = static_cast<uint32_t>(b % a.groups);
     b /= a.groups;
     const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);

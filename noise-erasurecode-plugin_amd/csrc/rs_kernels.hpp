@@ -38,6 +38,7 @@ struct MatArgs {
                                  // with all m rows (encode)
     const uint64_t* shard_ptrs;  // [stripe][k + m] device address of every shard (pointer
                                  // mode: data/parity/strides/pitch unused), or nullptr
+    uint32_t xcd;                // 1: XCD-aware block order (xcd.hpp)
 };
 
 // Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel

@@ -212,6 +212,8 @@ struct rs_ctx {
     const rsmi::BitsliceKernel* bitslice = nullptr;
     bool bitslice_rec = false;  // batched reconstruct uses bitslice->reconstruct ...
     int bitslice_rec_min_e = 1;  // ... for stripes with at least this many erasures
+    uint32_t xcd = 1;            // XCD-aware block order in the streaming kernels (RSMI_XCD) ...
+    uint32_t xcd_split_enc = 0;  // ... except the split-table encode (slower with it, profiles/r02ak/)
     std::string rec_name;        // rs_kernel_name(ctx, 1) when bitslice_rec
 
     // Immutable after rs_new: encode pattern (PatBlob layout, one pattern)
@@ -359,6 +361,7 @@ rsmi::MatArgs base_args(const rs_ctx* c, void* data, size_t dss, void* parity, s
     a.ncols16 = static_cast<uint32_t>(round_up(len, 16) / 16);
     a.k = static_cast<uint32_t>(c->k);
     a.m = static_cast<uint32_t>(c->m);
+    a.xcd = c->xcd;
     return a;
 }
 
@@ -379,7 +382,11 @@ const rsmi::BitsliceKernel* pick_bitslice(const std::vector<uint8_t>& enc, int k
 // Encode launch (all parity rows of every stripe): the generated bit-sliced
 // kernel when there is one for this code, else the split-table kernel.
 hipError_t launch_encode(const rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s) {
-    if (!c->bitslice) return rsmi::launch_matmul(a, c->m, s);
+    if (!c->bitslice) {
+        rsmi::MatArgs e = a;
+        e.xcd = c->xcd_split_enc;
+        return rsmi::launch_matmul(e, c->m, s);
+    }
     rsmi::BitsliceArgs b{};
     b.data = a.data;
     b.parity = a.parity;
@@ -389,6 +396,7 @@ hipError_t launch_encode(const rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s)
     b.stripes = a.stripes;
     b.ncols16 = a.ncols16;
     b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
+    b.xcd = a.xcd;
     return c->bitslice->launch(b, s);
 }
 
@@ -635,6 +643,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
         b.zpage = dev_zpage(c);
         b.shard_ptrs = shard_ptrs;
+        b.xcd = a.xcd;
         e = c->bitslice->reconstruct(b, s);
     }
     L.end(s);  // under pat_mu: an eviction waits for these launches
@@ -937,6 +946,16 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
                               ? std::string(c->bitslice->rec_name)
                               : std::string(rsmi::variant_name(k, std::min(c->m, c->bitslice_rec_min_e - 1))) + " (e<" +
                                     std::to_string(c->bitslice_rec_min_e) + ") + " + c->bitslice->rec_name;
+    }
+    {
+        // XCD-aware block order (xcd.hpp) for the bit-sliced encode and both
+        // reconstruct kernels; the split-table encode keeps the natural order
+        // (profiles/r02ak/: RS(64,16) encode -10% time, reconstructs -2..3%,
+        // RS(10,4) split-table encode +2%).  RSMI_XCD=0 / 1: off / on for
+        // every kernel (A/B runs).
+        const char* xv = std::getenv("RSMI_XCD");
+        c->xcd = (xv && std::atoi(xv) == 0) ? 0u : 1u;
+        c->xcd_split_enc = (xv && std::atoi(xv) == 1) ? 1u : 0u;
     }
     {
         // Pattern-cache bound (RSMI_PATTERN_CAP, for tests): 2^20 patterns,
