@@ -35,7 +35,7 @@ struct BitsliceArgs {
     uint64_t stripes;
     uint32_t ncols16;      // 16-byte columns per shard (ceil(S / 16))
     uint32_t blocks_per_stripe;
-    uint32_t xcd;          // 1: XCD-aware block order (xcd.hpp)
+    uint32_t xcd;          // XCD-aware block order (xcd.hpp): stripes per region, 0 = natural
 };
 
 using BitsliceLaunch = hipError_t (*)(const BitsliceArgs&, hipStream_t);
@@ -56,7 +56,7 @@ struct BitsliceRecArgs {
     uint32_t blocks_per_stripe;
     const uint8_t* zpage;        // 2 KiB (one wave window) loaded for absent inputs
     const uint64_t* shard_ptrs;  // [stripe][k + m] shard addresses (pointer mode), or nullptr
-    uint32_t xcd;                // 1: XCD-aware block order (xcd.hpp)
+    uint32_t xcd;                // XCD-aware block order (xcd.hpp): stripes per region, 0 = natural
 };
 
 using BitsliceRecLaunch = hipError_t (*)(const BitsliceRecArgs&, hipStream_t);

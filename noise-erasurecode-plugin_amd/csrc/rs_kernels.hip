@@ -118,8 +118,8 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     uint32_t* tw = reinterpret_cast<uint32_t*>(lds4);
     uint8_t** sptr = reinterpret_cast<uint8_t**>(tw + k * MG * 5);
 
-    // A stripe's chunks x row groups run on one XCD, in order (xcd.hpp).
-    uint64_t b = a.xcd ? xcd_block(blockIdx.x, a.chunks * a.groups, static_cast<uint32_t>(a.stripes)) : blockIdx.x;
+    // XCD-aware order (xcd.hpp): regions of a.xcd blocks per XCD in turn.
+    uint64_t b = a.xcd ? xcd_block(blockIdx.x, a.xcd, gridDim.x) : blockIdx.x;
     const uint32_t grp = static_cast<uint32_t>(b % a.groups);
     b /= a.groups;
     const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);
@@ -367,6 +367,7 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     const size_t lds = static_cast<size_t>(a.k) * ((v.MG + 3) / 4) * kStepWords * 4 + a.k * sizeof(void*);
     const uint64_t blocks = a.stripes * a.chunks * a.groups;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+    if (a.xcd == ~0u) a.xcd = a.chunks * a.groups;  // a stripe per XCD region
     hipLaunchKernelGGL(v.fn, dim3(static_cast<uint32_t>(blocks)), dim3(v.BT), lds, stream, a);
     return hipGetLastError();
 }

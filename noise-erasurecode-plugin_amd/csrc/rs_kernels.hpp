@@ -38,7 +38,8 @@ struct MatArgs {
                                  // with all m rows (encode)
     const uint64_t* shard_ptrs;  // [stripe][k + m] device address of every shard (pointer
                                  // mode: data/parity/strides/pitch unused), or nullptr
-    uint32_t xcd;                // 1: XCD-aware block order (xcd.hpp)
+    uint32_t xcd;                // XCD-aware block order (xcd.hpp): blocks per region, or 0
+                                 // (natural); ~0u = all of a stripe's blocks (set at launch)
 };
 
 // Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel

@@ -213,7 +213,7 @@ struct rs_ctx {
     bool bitslice_rec = false;  // batched reconstruct uses bitslice->reconstruct ...
     int bitslice_rec_min_e = 1;  // ... for stripes with at least this many erasures
     uint32_t xcd = 1;            // XCD-aware block order in the streaming kernels (RSMI_XCD) ...
-    uint32_t xcd_split_enc = 0;  // ... except the split-table encode (slower with it, profiles/r02ak/)
+    uint32_t xcd_split_enc = 0;  // ... split-table encode: blocks per region (0: natural order; RSMI_XCD_ENC_REGION)
     std::string rec_name;        // rs_kernel_name(ctx, 1) when bitslice_rec
 
     // Immutable after rs_new: encode pattern (PatBlob layout, one pattern)
@@ -361,7 +361,7 @@ rsmi::MatArgs base_args(const rs_ctx* c, void* data, size_t dss, void* parity, s
     a.ncols16 = static_cast<uint32_t>(round_up(len, 16) / 16);
     a.k = static_cast<uint32_t>(c->k);
     a.m = static_cast<uint32_t>(c->m);
-    a.xcd = c->xcd;
+    a.xcd = c->xcd ? ~0u : 0u;  // split-table kernel: a stripe per XCD region
     return a;
 }
 
@@ -396,7 +396,7 @@ hipError_t launch_encode(const rs_ctx* c, const rsmi::MatArgs& a, hipStream_t s)
     b.stripes = a.stripes;
     b.ncols16 = a.ncols16;
     b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
-    b.xcd = a.xcd;
+    b.xcd = c->xcd;
     return c->bitslice->launch(b, s);
 }
 
@@ -643,7 +643,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
         b.zpage = dev_zpage(c);
         b.shard_ptrs = shard_ptrs;
-        b.xcd = a.xcd;
+        b.xcd = c->xcd;
         e = c->bitslice->reconstruct(b, s);
     }
     L.end(s);  // under pat_mu: an eviction waits for these launches
@@ -955,7 +955,11 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         // every kernel (A/B runs).
         const char* xv = std::getenv("RSMI_XCD");
         c->xcd = (xv && std::atoi(xv) == 0) ? 0u : 1u;
-        c->xcd_split_enc = (xv && std::atoi(xv) == 1) ? 1u : 0u;
+        c->xcd_split_enc = (xv && std::atoi(xv) == 1) ? ~0u : 0u;
+        const char* rv = std::getenv("RSMI_XCD_ENC_REGION");  // A/B knob: blocks per XCD region
+        if (rv) c->xcd_split_enc = static_cast<uint32_t>(std::max(0, std::atoi(rv)));
+        const char* bv = std::getenv("RSMI_XCD_BS_STRIPES");  // A/B knob: stripes per region (bit-sliced)
+        if (bv && c->xcd) c->xcd = static_cast<uint32_t>(std::max(1, std::atoi(bv)));
     }
     {
         // Pattern-cache bound (RSMI_PATTERN_CAP, for tests): 2^20 patterns,

@@ -17,15 +17,19 @@
 
 namespace rsmi {
 
-// Logical block of hardware block b in a grid of items * per blocks.  A
-// bijection on [0, items * per): the last items % 8 items keep the natural
-// order (they are dispatched last either way).  Grids are < 2^31 blocks.
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t per, uint32_t items) {
-    const uint32_t full = (items & ~7u) * per;
+// Logical block of hardware block b in a grid of `total` blocks, with the
+// grid cut into regions of `region` consecutive logical blocks dealt to the
+// XCDs in turn: XCD x runs regions x, x + 8, x + 16, ... and each region's
+// blocks in order.  region = blocks per stripe gives every stripe to one XCD;
+// region = 1 is the natural order.  A bijection on [0, total): the tail that
+// does not fill 8 regions keeps the natural order (it is dispatched last
+// either way).  Grids are < 2^31 blocks.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t region, uint32_t total) {
+    const uint32_t full = total - total % (8u * region);
     if (b >= full) return b;
     const uint32_t x = b & 7u, i = b >> 3;
-    const uint32_t sl = i / per, c = i - sl * per;
-    return (sl * 8u + x) * per + c;
+    const uint32_t q = i / region;
+    return (q * 8u + x) * region + (i - q * region);
 }
 
 }  // namespace rsmi
