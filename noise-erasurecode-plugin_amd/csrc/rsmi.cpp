@@ -957,9 +957,9 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         c->xcd = (xv && std::atoi(xv) == 0) ? 0u : 1u;
         c->xcd_split_enc = (xv && std::atoi(xv) == 1) ? ~0u : 0u;
         const char* rv = std::getenv("RSMI_XCD_ENC_REGION");  // A/B knob: blocks per XCD region
-        if (rv) c->xcd_split_enc = static_cast<uint32_t>(std::max(0, std::atoi(rv)));
+        if (rv) c->xcd_split_enc = static_cast<uint32_t>(std::min(std::max(0, std::atoi(rv)), 1 << 20));
         const char* bv = std::getenv("RSMI_XCD_BS_STRIPES");  // A/B knob: stripes per region (bit-sliced)
-        if (bv && c->xcd) c->xcd = static_cast<uint32_t>(std::max(1, std::atoi(bv)));
+        if (bv && c->xcd) c->xcd = static_cast<uint32_t>(std::min(std::max(1, std::atoi(bv)), 64));
     }
     {
         // Pattern-cache bound (RSMI_PATTERN_CAP, for tests): 2^20 patterns,
