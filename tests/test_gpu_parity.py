@@ -851,3 +851,41 @@ def test_pattern_tables_grow_across_calls():
         assert torch.equal(data, d0) and torch.equal(parity, p0), call
     assert f.pattern_count() > 150000 and f.pattern_evictions() == 0
     f.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n,S", [(10, 14, 65536), (64, 80, 65536), (8, 14, 4096 + 48)])
+@pytest.mark.parametrize("stripes", [1, 7, 8, 9, 17, 64])
+def test_xcd_block_order_matches_natural(k, n, S, stripes):
+    """The XCD-aware block order (csrc/xcd.hpp) only renumbers blocks: for
+    stripe counts below, at and past multiples of 8 (the tail keeps the
+    natural order) encode and 1..m-erasure reconstruct give the same bytes
+    as the natural order (RSMI_XCD=0) and as the oracle, with the order
+    forced on every kernel (RSMI_XCD=1) and with a region of 3 blocks for
+    the split-table encode."""
+    m = n - k
+    fx = {"0": _fec_env(k, n, RSMI_XCD="0"), "1": _fec_env(k, n, RSMI_XCD="1"),
+          "r3": _fec_env(k, n, RSMI_XCD_ENC_REGION="3")}
+    rng = np.random.default_rng(stripes * 31 + k)
+    er = _erasures(rng, stripes, n, m)
+    data, parity = _dev_stripes(fx["0"], stripes, S, S, 5 + stripes)
+    E = oracle.fec_matrix(k, n)
+    hd = data.cpu().numpy()
+    want = [oracle.encode(E, k, n, hd[s * k * S:(s + 1) * k * S].tobytes()) for s in range(stripes)]
+    d0 = data.clone()
+    for name, f in fx.items():
+        parity.zero_()
+        f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+        f.sync()
+        hp = parity.cpu().numpy()
+        for s in range(stripes):
+            assert hp[s * m * S:(s + 1) * m * S].tobytes() == want[s], (name, s)
+        p0 = parity.clone()
+        dv, pv = data.view(stripes, k, S), parity.view(stripes, m, S)
+        dv[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0xA5
+        pv[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0x5A
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+        f.sync()
+        assert torch.equal(data, d0) and torch.equal(parity, p0), name
+    for f in fx.values():
+        f.close()
