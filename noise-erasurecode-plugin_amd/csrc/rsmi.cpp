@@ -214,6 +214,7 @@ struct rs_ctx {
     int bitslice_rec_min_e = 1;  // ... for stripes with at least this many erasures
     uint32_t xcd = 1;            // XCD-aware block order in the streaming kernels (RSMI_XCD) ...
     uint32_t xcd_split_enc = 0;  // ... split-table encode: blocks per region (0: natural order; RSMI_XCD_ENC_REGION)
+    uint32_t xcd_split_rec = ~0u;  // ... split-table reconstruct: blocks per region (~0u: a stripe; RSMI_XCD_REC_REGION)
     std::string rec_name;        // rs_kernel_name(ctx, 1) when bitslice_rec
 
     // Immutable after rs_new: encode pattern (PatBlob layout, one pattern)
@@ -361,7 +362,7 @@ rsmi::MatArgs base_args(const rs_ctx* c, void* data, size_t dss, void* parity, s
     a.ncols16 = static_cast<uint32_t>(round_up(len, 16) / 16);
     a.k = static_cast<uint32_t>(c->k);
     a.m = static_cast<uint32_t>(c->m);
-    a.xcd = c->xcd ? ~0u : 0u;  // split-table kernel: a stripe per XCD region
+    a.xcd = c->xcd_split_rec;  // split-table reconstruct: a stripe per XCD region by default
     return a;
 }
 
@@ -958,6 +959,9 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         c->xcd_split_enc = (xv && std::atoi(xv) == 1) ? ~0u : 0u;
         const char* rv = std::getenv("RSMI_XCD_ENC_REGION");  // A/B knob: blocks per XCD region
         if (rv) c->xcd_split_enc = static_cast<uint32_t>(std::min(std::max(0, std::atoi(rv)), 1 << 20));
+        c->xcd_split_rec = c->xcd ? ~0u : 0u;
+        const char* qv = std::getenv("RSMI_XCD_REC_REGION");  // A/B knob: blocks per XCD region
+        if (qv) c->xcd_split_rec = static_cast<uint32_t>(std::min(std::max(0, std::atoi(qv)), 1 << 20));
         const char* bv = std::getenv("RSMI_XCD_BS_STRIPES");  // A/B knob: stripes per region (bit-sliced)
         if (bv && c->xcd) c->xcd = static_cast<uint32_t>(std::min(std::max(1, std::atoi(bv)), 64));
     }
