@@ -364,7 +364,13 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     a.iters = std::min<uint32_t>(iters_cap, total_it);
     a.chunks = (total_it + a.iters - 1) / a.iters;
     a.groups = static_cast<uint32_t>((max_e + v.MG - 1) / v.MG);
-    const size_t lds = static_cast<size_t>(a.k) * ((v.MG + 3) / 4) * kStepWords * 4 + a.k * sizeof(void*);
+    size_t lds = static_cast<size_t>(a.k) * ((v.MG + 3) / 4) * kStepWords * 4 + a.k * sizeof(void*);
+    static const size_t lds_floor = [] {
+        const char* e = std::getenv("RSMI_LDS_PAD_KB");  // A/B knob: LDS per block >= this (caps occupancy)
+        const int kb = e ? std::atoi(e) : 0;
+        return static_cast<size_t>(kb > 0 && kb <= 64 ? kb : 0) * 1024;
+    }();
+    lds = std::max(lds, lds_floor);
     const uint64_t blocks = a.stripes * a.chunks * a.groups;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
     if (a.xcd == ~0u) a.xcd = a.chunks * a.groups;  // a stripe per XCD region
