@@ -512,6 +512,47 @@ def test_config2_full_size_64GiB_roundtrip():
     torch.cuda.empty_cache()
 
 
+def test_config5_full_size_roundtrip():
+    """BASELINE configs[4] at the bench's size: 16,384 RS(64,16) stripes x
+    80 x 64 KiB (64 GiB data + 16 GiB parity) through the bit-sliced encode
+    and the syndrome reconstruct in their XCD-aware block order.  Encode ->
+    oracle spot checks (first, middle, last stripe) -> erase 1-16 random
+    shards per stripe (a fresh pattern almost every stripe) -> reconstruct ->
+    torch.equal of all 80 GiB against a device clone."""
+    import bench
+    k, n, S, stripes = 64, 80, 1 << 16, 16384
+    m = n - k
+    free, _ = torch.cuda.mem_get_info()
+    need = 2 * stripes * n * S + (1 << 30)
+    if free < need:
+        pytest.skip(f"needs {need >> 30} GiB free on the device")
+    f = fec(k, n)
+    assert f.kernel_name(0).startswith("bitslice") and f.kernel_name(1).startswith("bitslice_rec")
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(data.data_ptr(), data.numel(), 0xC5)
+    f.fill_splitmix(parity.data_ptr(), parity.numel(), 2)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    E = oracle.fec_matrix(k, n)
+    for s in (0, stripes // 2 + 3, stripes - 1):
+        hd = data[s * k * S:(s + 1) * k * S].cpu().numpy().tobytes()
+        hp = parity[s * m * S:(s + 1) * m * S].cpu().numpy().tobytes()
+        assert hp == oracle.encode(E, k, n, hd), s
+    d0, p0 = data.clone(), parity.clone()
+    rng = np.random.default_rng(0xE4A6)
+    er = bench.erasure_sets(rng, 1, stripes, n, 1, m)[0]
+    data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+    parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                          er.tobytes())
+    f.sync()
+    assert torch.equal(data, d0)
+    assert torch.equal(parity, p0)
+    del data, parity, d0, p0
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_distributed_gather_and_pointer_reconstruct(world):
     """rsmi.distributed end to end on one GPU: the holder buffers of `world`
