@@ -68,6 +68,7 @@ struct BitsliceKernel {
     BitsliceLaunch launch;
     const char* rec_name;         // "bitslice_rec_k<k>_m<m>", or nullptr
     BitsliceRecLaunch reconstruct;  // nullptr when k > 64
+    int rec_iters;                  // 8 KiB column windows per reconstruct block (gen_bitslice -I)
 };
 
 // Generated kernel for encode of (k, k+m), or nullptr.

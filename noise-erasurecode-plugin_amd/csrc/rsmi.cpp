@@ -641,7 +641,9 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.dst = a.dst;
         b.dst_stride = a.dst_stride;
         b.ncols16 = a.ncols16;
-        b.blocks_per_stripe = (a.ncols16 + 511u) / 512u;  // 256 lanes x 2 columns per block
+        // 256 lanes x 2 columns per window, rec_iters windows per block
+        const uint32_t windows = (a.ncols16 + 511u) / 512u, it = static_cast<uint32_t>(c->bitslice->rec_iters);
+        b.blocks_per_stripe = (windows + it - 1u) / it;
         b.zpage = dev_zpage(c);
         b.shard_ptrs = shard_ptrs;
         b.xcd = c->xcd;
