@@ -24,7 +24,7 @@ namespace rsmi {
 // region = 1 is the natural order.  A bijection on [0, total): the tail that
 // does not fill 8 regions keeps the natural order (it is dispatched last
 // either way).  Grids are < 2^31 blocks.
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t region, uint32_t total) {
+__host__ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t region, uint32_t total) {
     const uint32_t full = total - total % (8u * region);
     if (b >= full) return b;
     const uint32_t x = b & 7u, i = b >> 3;

@@ -57,3 +57,15 @@ def test_shard_wire_fuzz_under_sanitizer():
     r = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "wire_fuzz: ok" in r.stdout
+
+
+def test_xcd_block_order_is_a_bijection():
+    """csrc/xcd.hpp's block renumbering, host build under
+    ASan/UBSan: a permutation of the grid for 165 (region, grid) sizes, each
+    full group of 8 regions spread one region per XCD, in order, and the
+    tail left in place."""
+    exe = os.path.join(BUILD, "xcd_check")
+    assert os.path.exists(exe), "run __graft_entry__.build() (make -C tests/capi)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "cases ok" in r.stdout
