@@ -36,6 +36,10 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, int iters, uint32_t m0, 
             if constexpr (KIND == 18) BODY("v_lshrrev_b32 %0, %1, %0");
             if constexpr (KIND == 19) BODY("v_or_b32 %0, %0, %1");
             if constexpr (KIND == 20) BODY("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8");
+            if constexpr (KIND == 21) BODY("v_pk_mul_lo_u16 %0, %0, 16");
+            if constexpr (KIND == 22) BODY("v_mul_u32_u24 %0, %0, 16");
+            if constexpr (KIND == 23) BODY("v_add3_u32 %0, %0, %0, %1");
+            if constexpr (KIND == 24) BODY("v_pk_add_u16 %0, %0, %0");
         }
     }
     uint32_t r = 0;
@@ -64,8 +68,9 @@ int main() {
     const char* names[] = {"v_xor_b32", "v_and_b32", "v_lshlrev_b32", "v_lshrrev_b32", "v_bfi_b32", "v_bitop3 (bfi)",
                            "v_bitop3 (xor3)", "v_perm_b32", "v_alignbit_b32", "v_lshl_or_b32", "v_and_or_b32",
                            "v_xor_b32_e64", "v_mov_b32", "v_lshlrev (vgpr amt)", "v_lshlrev_e64", "v_pk_lshlrev_b16",
-                           "v_add_u32 x+x", "v_lshl_add_u32", "v_lshrrev (vgpr)", "v_or_b32", "v_bitop3 (maj)"};
-    float ms[21];
+                           "v_add_u32 x+x", "v_lshl_add_u32", "v_lshrrev (vgpr)", "v_or_b32", "v_bitop3 (maj)",
+                           "v_pk_mul_lo_u16", "v_mul_u32_u24", "v_add3_u32", "v_pk_add_u16"};
+    float ms[25];
     ms[0] = run<0>(out, blocks, iters); ms[1] = run<1>(out, blocks, iters); ms[2] = run<2>(out, blocks, iters);
     ms[3] = run<3>(out, blocks, iters); ms[4] = run<4>(out, blocks, iters); ms[5] = run<5>(out, blocks, iters);
     ms[6] = run<6>(out, blocks, iters); ms[7] = run<7>(out, blocks, iters); ms[8] = run<8>(out, blocks, iters);
@@ -74,8 +79,10 @@ int main() {
     ms[13] = run<13>(out, blocks, iters); ms[14] = run<14>(out, blocks, iters); ms[15] = run<15>(out, blocks, iters);
     ms[16] = run<16>(out, blocks, iters); ms[17] = run<17>(out, blocks, iters); ms[18] = run<18>(out, blocks, iters);
     ms[19] = run<19>(out, blocks, iters); ms[20] = run<20>(out, blocks, iters);
+    ms[21] = run<21>(out, blocks, iters); ms[22] = run<22>(out, blocks, iters); ms[23] = run<23>(out, blocks, iters);
+    ms[24] = run<24>(out, blocks, iters);
     const double winstr = double(blocks) * 4 * iters * 8;
-    for (int i = 0; i < 21; ++i)
+    for (int i = 0; i < 25; ++i)
         printf("%-16s %.3f ms  %.3f wave-instr per SIMD per ns\n", names[i], ms[i], winstr / 1024 / (ms[i] * 1e6));
     return 0;
 }
