@@ -368,12 +368,14 @@ rsmi::MatArgs base_args(const rs_ctx* c, void* data, size_t dss, void* parity, s
 
 // Generated bit-sliced encode kernel for (k, m) if the build has one whose
 // embedded matrix is this context's.  By default it serves the codes whose
-// split-table encode is VALU-bound (k*m >= 256, e.g. RS(64,16)); the
-// RSMI_BITSLICE knob forces it on (1) or off (0) for A/B runs.
+// split-table encode does at least 3 MACs per byte moved, k*m >= 3(k+m):
+// RS(64,16) (12.8) and RS(8,14) (3.4, profiles/r02bq), not RS(10,4) (2.9,
+// at its movement ceiling either way).  The RSMI_BITSLICE knob forces it on
+// (1) or off (0) for A/B runs.
 const rsmi::BitsliceKernel* pick_bitslice(const std::vector<uint8_t>& enc, int k, int m) {
     const char* e = std::getenv("RSMI_BITSLICE");
     if (e && std::atoi(e) == 0) return nullptr;
-    if (!e && k * m < 256) return nullptr;
+    if (!e && k * m < 3 * (k + m)) return nullptr;
     const rsmi::BitsliceKernel* b = rsmi::bitslice_kernel(k, m);
     if (!b) return nullptr;
     const uint8_t* bottom = enc.data() + static_cast<size_t>(k) * k;

@@ -187,15 +187,18 @@ def _fec_with_env(k, n, bitslice):
 
 
 def test_bitslice_kernel_selection():
-    """The generated kernel serves RS(64,16) by default, RS(10,4) on request."""
+    """The generated kernel serves RS(64,16) and RS(8,14) by default, RS(10,4)
+    on request."""
     assert fec(64, 80).kernel_name(0) == "bitslice_k64_m16"
+    assert fec(8, 14).kernel_name(0) == "bitslice_k8_m6"
+    assert _fec_with_env(8, 14, "0").kernel_name(0).startswith("K8_MG6")
     assert fec(10, 14).kernel_name(0).startswith("K10_MG4")
     assert _fec_with_env(10, 14, "1").kernel_name(0) == "bitslice_k10_m4"
     assert _fec_with_env(64, 80, "0").kernel_name(0).startswith("K64_MG16")
     assert fec(17, 49).kernel_name(0).startswith("K0_")  # no generated kernel
 
 
-@pytest.mark.parametrize("k,n", [(64, 80), (10, 14)])
+@pytest.mark.parametrize("k,n", [(64, 80), (10, 14), (8, 14)])
 @pytest.mark.parametrize("S,pitch", [(16, 16), (17, 32), (1000, 1008), (8192, 8192),
                                      (8192 + 16, 8208), (65536, 65536), (100000, 100000)])
 def test_bitslice_encode_stripes_matches_oracle(k, n, S, pitch):
@@ -253,6 +256,8 @@ def test_bitslice_reconstruct_kernel_selection():
     assert fec(10, 14).kernel_name(1).startswith("K10_MG4")
     assert _fec_env(10, 14, RSMI_BITSLICE="1", RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == \
         "bitslice_rec_k10_m4"
+    assert fec(8, 14).kernel_name(1) == "bitslice_rec_k8_m6"
+    assert _fec_env(8, 14, RSMI_BITSLICE="0").kernel_name(1).startswith("K8_MG")
 
 
 def _fixed_patterns(k, n):
@@ -268,7 +273,7 @@ def _fixed_patterns(k, n):
     return out
 
 
-@pytest.mark.parametrize("k,n", [(64, 80), (10, 14)])
+@pytest.mark.parametrize("k,n", [(64, 80), (10, 14), (8, 14)])
 @pytest.mark.parametrize("S,pitch", [(16, 16), (17, 32), (1000, 1008), (8192 + 16, 8208),
                                      (65536, 65536), (100000, 100000)])
 def test_bitslice_reconstruct_roundtrip(k, n, S, pitch):
@@ -805,10 +810,12 @@ def test_host_api_pinned_buffers(k, n, S):
 def test_rs8_14_row_group_of_six(S, pitch):
     """RS(8,14) (infectious's example code) encodes with a 6-row group
     (K8_MG6: the last 4-row sub-step codes 2 rows) and reconstructs <= 4
-    erasures with K8_MG4: parity vs the oracle, round trip vs the originals."""
+    erasures with K8_MG4: parity vs the oracle, round trip vs the originals.
+    The split-table kernels are forced (RSMI_BITSLICE=0): by default this
+    code is bit-sliced (test_bitslice_*)."""
     k, n = 8, 14
     m = n - k
-    f = fec(k, n)
+    f = _fec_with_env(k, n, "0")
     assert f.kernel_name(0).startswith("K8_MG6")
     stripes = 9
     data, parity = _dev_stripes(f, stripes, S, pitch, 88 + S)

@@ -3,7 +3,7 @@
 //   map 0: logical block = b                 (default: a stripe's column chunks spread over all XCDs)
 //   map 1: logical block = (b % 8) * (G / 8) + b / 8   (each XCD streams one contiguous eighth)
 //   map 2: logical block = (b / 8) % C * ... chunk-major: chunk c of 8 consecutive stripes on one XCD
-// Shapes: RS(10,4) with 1 MiB shards (4 KiB per shard per block) and
+// Shapes: RS(10,4) and RS(8,14) with 1 MiB shards (4 KiB per shard per block) and
 // RS(64,16) with 64 KiB shards (8 KiB per shard per block), nt loads/stores.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -83,6 +83,7 @@ int main() {
     for (int rep = 0; rep < 2; ++rep) {
         shape<10, 4, 1>("RS(10,4) 1 MiB", 1 << 20, 4096, data, par);          // 40 GiB data
         shape<64, 16, 2>("RS(64,16) 64 KiB", 1 << 16, 8192, data, par);      // 32 GiB data
+        shape<8, 6, 1>("RS(8,14) 1 MiB", 1 << 20, 2048, data, par);          // 16 GiB data, 12 GiB parity
     }
     return 0;
 }
