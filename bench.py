@@ -19,8 +19,12 @@ data path -> weak scaling.  The driver launches N>1 with torch.distributed.run.
 Also reported: the roofline of the dominant kernel (encode, HIP events on the
 launch stream) against the 8 TB/s HBM3E peak, and the CPU baseline (the
 oracle's ports of infectious's scalar and split-nibble addmul, 1 thread and
-all usable CPUs, on a bounded sample of the same workload, rank 0 at N=1
-only).
+all usable CPUs, on a bounded sample of the same workload, on rank 0 after
+the timed region at every N).
+
+`--gpus N` with N > 1 and no launcher starts N ranks itself
+(torch.distributed.run as a child process, the JSON line relayed); under a
+launcher, WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
@@ -202,9 +206,74 @@ def emit(obj):
     out.flush()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(gpus: int, argv, port: int):
+    """The torch.distributed.run command that runs this script as `gpus`
+    ranks on this node (one per GPU), with every flag passed through."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus: int, env=None):
+    """How this process should run for `--gpus gpus`:
+      "single": one process, no launcher (N = 1);
+      "launch": no launcher set RANK and N > 1 -> start N ranks as a child;
+      "rank":   started by a launcher whose WORLD_SIZE matches --gpus.
+    A launcher world that disagrees with --gpus is an error (SystemExit 2),
+    so a record can never claim N GPUs while running another count."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if "WORLD_SIZE" in env or "RANK" in env:
+        world = int(env.get("WORLD_SIZE", "1"))
+        if world != gpus:
+            sys.stderr.write(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {gpus}\n")
+            raise SystemExit(2)
+        return "rank"
+    return "launch" if gpus > 1 else "single"
+
+
+def self_launch(gpus: int, argv) -> int:
+    """Runs N ranks under torch.distributed.run as a child process (never an
+    exec: this process has not touched the GPU, and must not replace itself
+    after any process has) and relays the one JSON line rank 0 prints.
+    Returns the child's exit code."""
+    import subprocess
+    cmd = launch_command(gpus, argv, _free_port())
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.stderr.write("bench.py: launching " + " ".join(cmd) + "\n")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = 0
+    for line in proc.stdout:
+        if line.lstrip().startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            lines += 1
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and lines != 1:
+        sys.stderr.write(f"bench.py: expected one JSON line from rank 0, got {lines}\n")
+        return 1
+    return rc
+
+
 def main():
     global _RESULT_OUT
     args = parse()
+    how = check_world(args.gpus)
+    if how == "launch":
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
     sys.stdout.flush()
     _RESULT_OUT = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
@@ -214,6 +283,10 @@ def main():
     # RSMI_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a
     # device round-robin; the driver's runs use RCCL, one rank per GPU).
     backend = os.environ.get("RSMI_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and world > torch.cuda.device_count():
+        sys.stderr.write(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPUs visible "
+                         "(RSMI_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)\n")
+        raise SystemExit(2)
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
@@ -337,7 +410,7 @@ def main():
     local_bytes = step_bytes_local
     if rank == 0:
         cpu = None
-        if world == 1 and args.cpu_seconds > 0:
+        if args.cpu_seconds > 0:  # after the timed region, on rank 0, at every N
             cpu = cpu_baseline(k, n, S, args.cpu_seconds, args.cpu_threads)
         out = {
             "metric": "RS(10,4) encode+reconstruct GB/s at 1/8 GPUs; % HBM roofline",

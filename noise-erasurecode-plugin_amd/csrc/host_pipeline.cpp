@@ -117,38 +117,47 @@ HostPipeline::HostPipeline() : pool_(CopyPool::shared()) {}
 HostPipeline::~HostPipeline() {
     for (Slot& s : slots_) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.d_in) (void)hipFreeAsync(s.d_in, s.stream);
+        if (s.d_out) (void)hipFreeAsync(s.d_out, s.stream);
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.h_in) (void)hipHostFree(s.h_in);
         if (s.h_out) (void)hipHostFree(s.h_out);
-        if (s.d_in) (void)hipFree(s.d_in);
-        if (s.d_out) (void)hipFree(s.d_out);
+        for (uint8_t* r : s.retired) (void)hipHostFree(r);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.stream) (void)hipStreamDestroy(s.stream);
     }
 }
 
+// Grows one side of a slot (its previous chunk was drained, and all its
+// device work ran on s.stream): the device buffer is replaced in stream order
+// (hipFreeAsync / hipMallocAsync, no sync), the pinned one is retired until
+// the pipeline is destroyed (hipHostFree would sync the whole device).  x2
+// growth bounds both the number of growths and the retired bytes.
+bool HostPipeline::grow(Slot& s, uint8_t** h, uint8_t** d, size_t* cap, size_t bytes) {
+    const size_t want = std::max(bytes, 2 * *cap);
+    uint8_t* nh = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&nh), want, hipHostMallocDefault) != hipSuccess) return false;
+    if (*d && hipFreeAsync(*d, s.stream) != hipSuccess) {
+        (void)hipHostFree(nh);
+        return false;
+    }
+    *d = nullptr;
+    if (*h) s.retired.push_back(*h);
+    *h = nh;
+    *cap = 0;
+    if (hipMallocAsync(reinterpret_cast<void**>(d), want, s.stream) != hipSuccess) {
+        *d = nullptr;
+        return false;
+    }
+    *cap = want;
+    return true;
+}
+
 bool HostPipeline::ensure(Slot& s, size_t in_bytes, size_t out_bytes) {
     if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return false;
     if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return false;
-    if (in_bytes > s.cap_in) {
-        if (s.h_in) (void)hipHostFree(s.h_in);
-        if (s.d_in) (void)hipFree(s.d_in);
-        s.h_in = s.d_in = nullptr;
-        s.cap_in = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_in), in_bytes, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.d_in), in_bytes) != hipSuccess)
-            return false;
-        s.cap_in = in_bytes;
-    }
-    if (out_bytes > s.cap_out) {
-        if (s.h_out) (void)hipHostFree(s.h_out);
-        if (s.d_out) (void)hipFree(s.d_out);
-        s.h_out = s.d_out = nullptr;
-        s.cap_out = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&s.h_out), out_bytes, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&s.d_out), out_bytes) != hipSuccess)
-            return false;
-        s.cap_out = out_bytes;
-    }
+    if (in_bytes > s.cap_in && !grow(s, &s.h_in, &s.d_in, &s.cap_in, in_bytes)) return false;
+    if (out_bytes > s.cap_out && !grow(s, &s.h_out, &s.d_out, &s.cap_out, out_bytes)) return false;
     return true;
 }
 

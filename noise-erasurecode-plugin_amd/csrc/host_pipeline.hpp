@@ -89,8 +89,10 @@ private:
         size_t cap_in = 0, cap_out = 0;
         bool pending = false;
         size_t c0 = 0, w = 0, pitch = 0;
+        std::vector<uint8_t*> retired;  // outgrown pinned buffers, freed with the pipeline
     };
     bool ensure(Slot& s, size_t in_bytes, size_t out_bytes);
+    bool grow(Slot& s, uint8_t** h, uint8_t** d, size_t* cap, size_t bytes);
     hipError_t drain(Slot& s, uint8_t* const* dsts, int e);
     Slot slots_[kSlots];
     CopyPool& pool_;

@@ -61,6 +61,20 @@ void PatIndex::clear() {
     size_ = 0;
 }
 
+void PatIndex::drop_from(int first_id) {
+    // Linear probing cannot leave holes inside a probe run, so the kept
+    // entries are reinserted into a cleared table of the same size.
+    std::vector<PatKey> keys;
+    std::vector<int32_t> ids;
+    for (size_t s = 0; s < ids_.size(); ++s)
+        if (ids_[s] >= 0 && ids_[s] < first_id) {
+            keys.push_back(keys_[s]);
+            ids.push_back(ids_[s]);
+        }
+    clear();
+    for (size_t i = 0; i < ids.size(); ++i) insert(keys[i], ids[i]);
+}
+
 void PatIndex::rehash(size_t cap) {
     std::vector<PatKey> keys(cap);
     std::vector<int32_t> ids(cap, -1);

@@ -38,6 +38,8 @@ public:
     // Adds key -> id; the key must be absent.
     void insert(const PatKey& key, int id);
     void clear();
+    // Removes every entry whose id is >= first_id (a failed build's patterns).
+    void drop_from(int first_id);
     size_t size() const { return size_; }
 
 private:

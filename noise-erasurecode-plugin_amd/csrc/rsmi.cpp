@@ -46,71 +46,106 @@ struct DeviceGuard {
     }
 };
 
-// A growable device buffer.  Growing synchronises the device first, since
-// earlier launches may still read the old allocation.
+// A growable device buffer.  reserve() is for buffers sized once (the
+// context's immutable tables, at rs_new).  reserve_on() is stream-ordered
+// (hipMallocAsync / hipFreeAsync on s): the caller has ordered s after every
+// earlier user of the buffer (a lease's begin()), so the outgrown allocation
+// is freed on the device timeline with no host or device-wide sync -- a
+// caller whose request outgrows the buffer never stalls the others (hipFree
+// would: it implies a hipDeviceSynchronize).
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    bool stream_ordered = false;  // allocated by reserve_on
     bool reserve(size_t bytes) {
         if (bytes <= cap) return true;
-        if (p) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(p);
+        release();
+        size_t want = std::max(bytes, size_t(4096));
+        if (hipMalloc(&p, want) != hipSuccess) {
             p = nullptr;
-            cap = 0;
+            return false;
         }
-        size_t want = std::max({bytes, size_t(4096), 2 * cap});
-        if (hipMalloc(&p, want) != hipSuccess) return false;
         cap = want;
         return true;
     }
+    bool reserve_on(size_t bytes, hipStream_t s) {
+        if (bytes <= cap) return true;
+        const size_t want = std::max({bytes, size_t(4096), 2 * cap});
+        if (p) {
+            if ((stream_ordered ? hipFreeAsync(p, s) : hipFree(p)) != hipSuccess) return false;
+            p = nullptr;
+            cap = 0;
+        }
+        if (hipMallocAsync(&p, want, s) != hipSuccess) {
+            p = nullptr;
+            return false;
+        }
+        cap = want;
+        stream_ordered = true;
+        return true;
+    }
+    // Callers have drained every user of the buffer (rs_free / lease
+    // teardown); the stream of the allocation may be gone (a caller's), so a
+    // stream-ordered buffer is freed on the null stream.
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (stream_ordered) {
+                (void)hipFreeAsync(p, nullptr);
+                (void)hipStreamSynchronize(nullptr);
+            } else {
+                (void)hipFree(p);
+            }
+        }
         p = nullptr;
         cap = 0;
+        stream_ordered = false;
     }
 };
 
-// A growable device buffer whose first `used` bytes survive growth.
+// A growable device buffer whose first `used` bytes survive growth, read by
+// launches on many streams (the pattern tables).  Growth is stream-ordered on
+// the build stream s, which the caller has first ordered after the last
+// launch of every lease (order_after_readers): the old allocation is copied
+// and then freed on s, never by a host-side sync.
 struct GrowBuf {
     void* p = nullptr;
     size_t cap = 0;
-    // Outgrown buffers.  Launches enqueued before a growth (on any lease's
-    // stream) may still read them, so they are kept until release() instead
-    // of a device-wide sync here; x4 growth keeps them under 1/3 of `cap`.
-    std::vector<void*> retired;
-    // Grows to hold `bytes`, keeping the first `used` bytes (copied on s,
-    // which the caller has ordered after their last writer).
     bool reserve_keep(size_t bytes, size_t used, hipStream_t s) {
         if (bytes <= cap) return true;
         const size_t want = std::max({bytes, size_t(4096), 4 * cap});
         void* np = nullptr;
-        if (hipMalloc(&np, want) != hipSuccess) return false;
+        if (hipMallocAsync(&np, want, s) != hipSuccess) return false;
         if (p && used &&
             hipMemcpyAsync(np, p, std::min(used, cap), hipMemcpyDeviceToDevice, s) != hipSuccess) {
-            (void)hipFree(np);
+            (void)hipFreeAsync(np, s);
             return false;
         }
-        if (p) retired.push_back(p);
+        if (p) (void)hipFreeAsync(p, s);
         p = np;
         cap = want;
         return true;
     }
-    void release() {
-        for (void* r : retired) (void)hipFree(r);
-        retired.clear();
-        if (p) (void)hipFree(p);
+    bool needs(size_t bytes) const { return bytes > cap; }
+    void release() {  // every reader drained (rs_free)
+        if (p) {
+            (void)hipFreeAsync(p, nullptr);
+            (void)hipStreamSynchronize(nullptr);
+        }
         p = nullptr;
         cap = 0;
     }
 };
 
 // Pinned host staging whose reuse waits for the copies that read it.
+// Growth never frees on the hot path (hipHostFree implies a device-wide
+// sync): the outgrown buffer is retired and freed at destroy(); growth is
+// x2, so the retired buffers never exceed the live one.
 struct Staging {
     void* p = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
+    std::vector<void*> retired;
     bool acquire(size_t bytes) {
         if (pending) {
             (void)hipEventSynchronize(done);
@@ -118,11 +153,11 @@ struct Staging {
         }
         if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) return false;
         if (bytes <= cap) return true;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max(bytes, size_t(1) << 16);
-        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return false;
+        const size_t want = std::max({bytes, size_t(1) << 16, 2 * cap});
+        void* np = nullptr;
+        if (hipHostMalloc(&np, want, hipHostMallocDefault) != hipSuccess) return false;
+        if (p) retired.push_back(p);
+        p = np;
         cap = want;
         return true;
     }
@@ -131,6 +166,8 @@ struct Staging {
     }
     void destroy() {
         if (pending) (void)hipEventSynchronize(done);
+        for (void* r : retired) (void)hipHostFree(r);
+        retired.clear();
         if (p) (void)hipHostFree(p);
         if (done) (void)hipEventDestroy(done);
         p = nullptr;
@@ -167,6 +204,7 @@ struct Lease {
     std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
     std::vector<uint32_t> pid, start;          // reconstruct scratch
     std::vector<uint64_t> sort_a, sort_b;      // (bucket, stripe) radix-sort scratch
+    std::vector<PatKey> miss_keys;             // distinct new patterns of a call
 
     bool init() {
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
@@ -237,6 +275,7 @@ struct rs_ctx {
     GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat, d_pkey;
     size_t uploaded = 0;    // patterns built on the device
     size_t pat_cap = 0;     // soft bound; reaching it evicts the whole cache
+    int test_fail_flush = 0, flush_attempts = 0;  // RSMI_TEST_FAIL_FLUSH (tests)
     uint64_t evictions = 0;
     std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
     std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
@@ -431,46 +470,83 @@ int create_pattern(rs_ctx* c, const PatKey& key, int e) {
 
 constexpr uint32_t kMissing = 0xFFFFFFFFu;
 
+void rollback_patterns(rs_ctx* c);
+
 // Pattern id of every stripe into pid.  With `create` (pat_mu exclusive)
-// missing patterns are added; without (pat_mu shared) they are counted in
-// *missing and their pid is kMissing.  With `only_missing`, stripes whose
-// pid is already set are skipped (the exclusive pass after a shared one).
-// More than m erasures in a stripe -> RS_ENOT_ENOUGH.
+// missing patterns are added (and rolled back if the call fails); without
+// (pat_mu shared) they are counted in *missing -- distinct patterns, so the
+// eviction check is not inflated by stripes sharing one new pattern -- and
+// their pid is kMissing.  A pattern not yet built (id >= uploaded) counts as
+// missing too.  With `only_missing`, stripes whose pid is already set are
+// skipped (the exclusive pass after a shared one).  More than m erasures in a
+// stripe -> RS_ENOT_ENOUGH.
 int lookup_patterns(rs_ctx* c, const uint8_t* erased, size_t stripes, std::vector<uint32_t>& pid,
-                    bool create, size_t* missing, bool only_missing = false) {
+                    bool create, size_t* missing, bool only_missing = false,
+                    std::vector<PatKey>* miss_keys = nullptr) {
     if (!only_missing) pid.assign(stripes, kMissing);
+    if (miss_keys) miss_keys->clear();
     size_t miss = 0;
     for (size_t i = 0; i < stripes; ++i) {
         if (only_missing && pid[i] != kMissing) continue;
         int e = 0;
         const PatKey key = rsmi::pattern_key(erased + i * c->n, c->n, &e);
-        if (e > c->m) return RS_ENOT_ENOUGH;
+        if (e > c->m) {
+            if (create) rollback_patterns(c);
+            return RS_ENOT_ENOUGH;
+        }
         const int id = c->pat_index.find(key);
-        if (id >= 0) {
+        if (id >= 0 && (create || static_cast<size_t>(id) < c->uploaded)) {
             pid[i] = static_cast<uint32_t>(id);
         } else if (create) {
             pid[i] = static_cast<uint32_t>(create_pattern(c, key, e));
         } else {
+            pid[i] = kMissing;
             ++miss;
+            if (miss_keys) miss_keys->push_back(key);
         }
     }
-    if (missing) *missing = miss;
+    if (missing) {
+        if (miss_keys && !miss_keys->empty()) {
+            std::vector<PatKey>& mk = *miss_keys;
+            auto lt = [](const PatKey& a, const PatKey& b) {
+                return std::lexicographical_compare(a.w, a.w + 4, b.w, b.w + 4);
+            };
+            std::sort(mk.begin(), mk.end(), lt);
+            miss = static_cast<size_t>(std::unique(mk.begin(), mk.end()) - mk.begin());
+        }
+        *missing = miss;
+    }
     return RS_OK;
 }
 
+// Orders the build stream after the last launch of every lease (pat_mu
+// exclusive): every launch that reads the pattern tables recorded its lease's
+// event while holding pat_mu, so this covers all of them -- on the device,
+// without a host sync.
+void order_after_readers(rs_ctx* c) {
+    std::lock_guard<std::mutex> lk(c->lease_mu);
+    for (const std::unique_ptr<Lease>& L : c->leases) L->begin(c->build_stream);
+}
+
 // Drops every cached pattern (pat_mu exclusive) without a host sync: the
-// build stream waits on the device for the last launch of every lease -- all launches that read the tables recorded their lease's
-// event while holding pat_mu -- before it overwrites rows.
+// build stream waits for every reader before it overwrites rows.
 void evict_patterns(rs_ctx* c) {
-    {
-        std::lock_guard<std::mutex> lk(c->lease_mu);
-        for (const std::unique_ptr<Lease>& L : c->leases) L->begin(c->build_stream);
-    }
+    order_after_readers(c);
     c->pat_index.clear();
     c->h_key.clear();
     c->h_cnt.clear();
     c->uploaded = 0;
     ++c->evictions;
+}
+
+// Undoes the patterns created since the last successful build (pat_mu
+// exclusive): after a failed lookup or build they must not stay in the index,
+// or a later call would find them and launch on rows never written.
+void rollback_patterns(rs_ctx* c) {
+    if (c->h_cnt.size() == c->uploaded) return;
+    c->pat_index.drop_from(static_cast<int>(c->uploaded));
+    c->h_cnt.resize(c->uploaded);
+    c->h_key.clear();
 }
 
 const uint8_t* dev_enc(const rs_ctx* c) { return static_cast<const uint8_t*>(c->d_gf.p); }
@@ -491,13 +567,19 @@ void wait_patterns(rs_ctx* c, hipStream_t s) {
 // context's build stream, in order (growth copies included), so a build can
 // overlap the kernels already queued on the callers' streams; readers wait
 // for pat_ev (wait_patterns).
-int flush_patterns(rs_ctx* c) {
+int flush_patterns_impl(rs_ctx* c) {
     const size_t npat = c->h_cnt.size(), first = c->uploaded;
     if (npat == first) return RS_OK;
+    if (npat > (size_t(1) << 24)) return RS_EINVAL;  // 24-bit ids in the stripe descriptors
     const hipStream_t s = c->build_stream;
     const size_t k = c->k, m = c->m, ds = dst_stride(c);
     const size_t cnt = npat - first, b_key = cnt * sizeof(PatKey);
     if (c->h_key.size() != cnt) return RS_EINVAL;  // internal invariant
+    // Growth frees the outgrown tables on the build stream: order it after
+    // every launch that may still read them first.
+    if (c->d_pcoef.needs(npat * m * k) || c->d_psrc.needs(npat * k * 4) || c->d_pdst.needs(npat * ds * 4) ||
+        c->d_pcnt.needs(npat * 4) || c->d_pstat.needs(npat * 4))
+        order_after_readers(c);
     if (!c->d_pcoef.reserve_keep(npat * m * k, first * m * k, s) ||
         !c->d_psrc.reserve_keep(npat * k * 4, first * k * 4, s) ||
         !c->d_pdst.reserve_keep(npat * ds * 4, first * ds * 4, s) ||
@@ -534,6 +616,22 @@ int flush_patterns(rs_ctx* c) {
     c->uploaded = npat;
     c->h_key.clear();
     return RS_OK;
+}
+
+// Test hook (RSMI_TEST_FAIL_FLUSH=N at rs_new): the context's N-th build
+// attempt fails with RS_ENOMEM before touching the device, as an allocation
+// would.
+bool injected_flush_failure(rs_ctx* c) {
+    return c->test_fail_flush > 0 && ++c->flush_attempts == c->test_fail_flush;
+}
+
+// Builds the pending patterns; on any failure they are rolled back, so the
+// cache only ever holds patterns whose rows were built (a retry recreates
+// them).
+int flush_patterns(rs_ctx* c) {
+    const int st = c->h_cnt.size() != c->uploaded && injected_flush_failure(c) ? RS_ENOMEM : flush_patterns_impl(c);
+    if (st != RS_OK) rollback_patterns(c);
+    return st;
 }
 
 void set_cache_patterns(const rs_ctx* c, rsmi::MatArgs& a) {
@@ -613,7 +711,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     }
     L.begin(s);  // the descriptor buffer's previous readers
     wait_patterns(c, s);
-    if (!L.d_stripe_pat.reserve(used * sizeof(uint2))) return RS_ENOMEM;
+    if (!L.d_stripe_pat.reserve_on(used * sizeof(uint2), s)) return RS_ENOMEM;
     hipError_t e = hipMemcpyAsync(L.d_stripe_pat.p, desc, used * sizeof(uint2), hipMemcpyHostToDevice, s);
     L.st_stripe.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
@@ -664,14 +762,16 @@ int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_
     uint64_t gen = 0;
     {
         std::shared_lock<std::shared_mutex> rl(c->pat_mu);
-        const int rc = lookup_patterns(c, erased, stripes, L.pid, false, &missing);
+        const int rc = lookup_patterns(c, erased, stripes, L.pid, false, &missing, false, &L.miss_keys);
         if (rc != RS_OK) return rc;
         if (missing == 0) return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, shard_ptrs, s);
         gen = c->evictions;
     }
     std::unique_lock<std::shared_mutex> wl(c->pat_mu);
     // Only the stripes the shared pass missed are looked up again, unless
-    // the cache was evicted meanwhile (ids found then are stale).
+    // the cache was evicted meanwhile (ids found then are stale).  `missing`
+    // counts distinct new patterns (an upper bound: another caller may have
+    // created some of them since).
     bool stale = c->evictions != gen;
     if (c->pat_index.size() + missing > c->pat_cap) {
         evict_patterns(c);
@@ -679,7 +779,6 @@ int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_
     }
     const int rc = lookup_patterns(c, erased, stripes, L.pid, true, nullptr, !stale);
     if (rc != RS_OK) return rc;
-    if (c->pat_index.size() > (size_t(1) << 24)) return RS_EINVAL;  // 24-bit ids in the descriptors
     const int st = flush_patterns(c);
     if (st != RS_OK) return st;
     return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, shard_ptrs, s);
@@ -708,7 +807,7 @@ int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vecto
         std::vector<uint8_t> hp(PatLayout(c, 1).total);
         pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
         // The previous pass's launches were drained by pipe->run.
-        if (!L.d_onepat.reserve(hp.size())) return RS_ENOMEM;
+        if (!L.d_onepat.reserve_on(hp.size(), L.stream)) return RS_ENOMEM;
         if (hipMemcpyAsync(L.d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice, L.stream) != hipSuccess ||
             hipStreamSynchronize(L.stream) != hipSuccess)
             return RS_EDEVICE;
@@ -740,7 +839,7 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
     if (!din || !dout) return false;
     const hipStream_t s = L.stream;
     L.begin(s);
-    if (!L.st_pieces.acquire(n * sizeof(uint64_t)) || !L.d_pieces.reserve(n * sizeof(uint64_t))) {
+    if (!L.st_pieces.acquire(n * sizeof(uint64_t)) || !L.d_pieces.reserve_on(n * sizeof(uint64_t), s)) {
         *rc = RS_ENOMEM;
         return true;
     }
@@ -974,6 +1073,8 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         // 1.3 GiB of tables for RS(64,16).
         const char* pc = std::getenv("RSMI_PATTERN_CAP");
         c->pat_cap = pc ? static_cast<size_t>(std::max(1, std::atoi(pc))) : (size_t(1) << 20);
+        const char* ff = std::getenv("RSMI_TEST_FAIL_FLUSH");
+        c->test_fail_flush = ff ? std::atoi(ff) : 0;
         const char* ml = std::getenv("RSMI_MAX_LEASES");
         c->max_leases = ml ? static_cast<size_t>(std::max(1, std::atoi(ml))) : 16;
     }
@@ -1092,8 +1193,11 @@ int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count)
     const hipStream_t s = lg.L->stream;
     std::unique_lock<std::shared_mutex> wl(c->pat_mu);
     std::vector<uint32_t> pid;
-    if (c->pat_index.size() + 1 > c->pat_cap) evict_patterns(c);
-    int st = lookup_patterns(c, erased, 1, pid, true, nullptr);
+    size_t missing = 0;
+    int st = lookup_patterns(c, erased, 1, pid, false, &missing);
+    if (st != RS_OK) return st;
+    if (missing && c->pat_index.size() + 1 > c->pat_cap) evict_patterns(c);
+    st = lookup_patterns(c, erased, 1, pid, true, nullptr);
     if (st != RS_OK) return st;
     st = flush_patterns(c);
     if (st != RS_OK) return st;
@@ -1119,25 +1223,39 @@ int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
     if (!g.ok) return RS_EDEVICE;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     std::unique_lock<std::shared_mutex> wl(c->pat_mu);
-    if (c->pat_index.size() + static_cast<size_t>(total) > c->pat_cap) evict_patterns(c);
     std::vector<uint8_t> er(c->n);
     std::vector<uint32_t> pid;
     std::vector<int> idx;
-    for (int e = 1; e <= max_e; ++e) {
-        idx.resize(e);
-        for (int i = 0; i < e; ++i) idx[i] = i;
-        while (true) {
-            std::fill(er.begin(), er.end(), 0);
-            for (int v : idx) er[v] = 1;
-            const int err = lookup_patterns(c, er.data(), 1, pid, true, nullptr);
-            if (err != RS_OK) return err;
-            int i = e - 1;
-            while (i >= 0 && idx[i] == c->n - e + i) --i;
-            if (i < 0) break;
-            ++idx[i];
-            for (int j = i + 1; j < e; ++j) idx[j] = idx[j - 1] + 1;
+    // Every pattern of 1..max_e erasures, in lexicographic order of ids.
+    auto for_each_pattern = [&](auto&& fn) -> int {
+        for (int e = 1; e <= max_e; ++e) {
+            idx.resize(e);
+            for (int i = 0; i < e; ++i) idx[i] = i;
+            while (true) {
+                std::fill(er.begin(), er.end(), 0);
+                for (int v : idx) er[v] = 1;
+                const int err = fn();
+                if (err != RS_OK) return err;
+                int i = e - 1;
+                while (i >= 0 && idx[i] == c->n - e + i) --i;
+                if (i < 0) break;
+                ++idx[i];
+                for (int j = i + 1; j < e; ++j) idx[j] = idx[j - 1] + 1;
+            }
         }
-    }
+        return RS_OK;
+    };
+    // Evict only when the patterns not cached yet would pass the cap.
+    size_t absent = 0;
+    (void)for_each_pattern([&] {
+        size_t miss = 0;
+        const int err = lookup_patterns(c, er.data(), 1, pid, false, &miss);
+        absent += miss;
+        return err;
+    });
+    if (absent && c->pat_index.size() + absent > c->pat_cap) evict_patterns(c);
+    const int err = for_each_pattern([&] { return lookup_patterns(c, er.data(), 1, pid, true, nullptr); });
+    if (err != RS_OK) return err;
     const int st = flush_patterns(c);
     if (st != RS_OK) return st;
     return pattern_status(c, 0, c->h_cnt.size(), s);  // synchronises s
@@ -1379,8 +1497,8 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     L.begin(s);  // the lease's buffers may last have been read on another stream
     const size_t table_bytes = B * static_cast<size_t>(n) * sizeof(uint64_t);
     if (!L.st_batch.acquire(std::max<size_t>(std::max(packed, E * pitch), 16)) ||
-        (packed && !L.d_pack.reserve(packed)) || !L.d_batch.reserve(std::max<size_t>(out_rows, 1) * pitch) ||
-        !L.st_pieces.acquire(table_bytes) || !L.d_pieces.reserve(table_bytes))
+        (packed && !L.d_pack.reserve_on(packed, s)) || !L.d_batch.reserve_on(std::max<size_t>(out_rows, 1) * pitch, s) ||
+        !L.st_pieces.acquire(table_bytes) || !L.d_pieces.reserve_on(table_bytes, s))
         return RS_ENOMEM;
     // From the first async copy on, every exit waits for the stream: the
     // staging buffers may not be reused (or freed) while a DMA reads them.
@@ -1507,8 +1625,8 @@ int rs_blake2b_batch(rs_ctx* c, int count, const uint8_t* const* msgs, const siz
     if (!pipe) return RS_ENOMEM;
     const hipStream_t s = L.stream;
     L.begin(s);
-    if (!L.st_batch.acquire(std::max<size_t>(total, 16)) || !L.d_batch.reserve(std::max<size_t>(total, 16)) ||
-        !L.st_pieces.acquire(desc_bytes + dig_bytes) || !L.d_pieces.reserve(desc_bytes + dig_bytes))
+    if (!L.st_batch.acquire(std::max<size_t>(total, 16)) || !L.d_batch.reserve_on(std::max<size_t>(total, 16), s) ||
+        !L.st_pieces.acquire(desc_bytes + dig_bytes) || !L.d_pieces.reserve_on(desc_bytes + dig_bytes, s))
         return RS_ENOMEM;
     auto finish = [&](int code) {
         if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;

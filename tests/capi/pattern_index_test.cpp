@@ -87,6 +87,16 @@ int main() {
             const PatKey k{{rng(), rng(), rng(), rng()}};
             CHECK(idx.find(k) == (ref.count(k) ? ref.at(k) : -1), "miss");
         }
+        // drop_from (a failed build's rollback): ids >= cut vanish, the rest
+        // stay findable, and dropped keys can be inserted again.
+        const int cut = static_cast<int>(ref.size()) * 2 / 3;
+        idx.drop_from(cut);
+        CHECK(idx.size() == static_cast<size_t>(cut), "drop_from size %zu vs %d", idx.size(), cut);
+        for (const PatKey& k : keys) CHECK(idx.find(k) == (ref.at(k) < cut ? ref.at(k) : -1), "after drop_from");
+        for (const PatKey& k : keys)
+            if (ref.at(k) >= cut) idx.insert(k, ref.at(k));
+        CHECK(idx.size() == ref.size(), "reinsert size");
+        for (const PatKey& k : keys) CHECK(idx.find(k) == ref.at(k), "lookup after reinsert");
         idx.clear();
         CHECK(idx.size() == 0, "clear");
         for (const PatKey& k : keys) CHECK(idx.find(k) == -1, "found after clear");

@@ -2,6 +2,7 @@
 the pattern count that decides up-front preparation, the CPU description and
 the cpu_baseline leg structure (the oracle timed on a tiny sample).  The GPU
 line itself is produced by the driver on an MI355X."""
+import os
 import sys
 
 import numpy as np
@@ -67,3 +68,47 @@ def test_parse_stream_mode(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--stream", "--stream-chunk", "16"])
     a = bench.parse()
     assert a.stream and a.stream_chunk == 16
+
+
+def test_check_world_modes():
+    """--gpus N decides how bench.py runs: one process at N = 1, a self-launch
+    of N ranks with no launcher, and a rank under a launcher whose WORLD_SIZE
+    must equal --gpus (a mismatch exits non-zero rather than recording the
+    wrong GPU count)."""
+    assert bench.check_world(1, {}) == "single"
+    assert bench.check_world(8, {}) == "launch"
+    assert bench.check_world(8, {"WORLD_SIZE": "8", "RANK": "3"}) == "rank"
+    assert bench.check_world(1, {"WORLD_SIZE": "1", "RANK": "0"}) == "rank"
+    for gpus, env in ((8, {"WORLD_SIZE": "1", "RANK": "0"}), (1, {"WORLD_SIZE": "2", "RANK": "1"}),
+                      (2, {"RANK": "0"})):
+        with pytest.raises(SystemExit) as ei:
+            bench.check_world(gpus, env)
+        assert ei.value.code == 2
+    with pytest.raises(SystemExit):
+        bench.check_world(0, {})
+
+
+def test_launch_command_passes_every_flag():
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5", "--placement", "sharded", "--erase", "0,1"]
+    cmd = bench.launch_command(8, argv, 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    i = cmd.index(os.path.abspath(bench.__file__))
+    assert cmd[i + 1:] == argv
+
+
+def test_self_launch_relays_one_json_line(monkeypatch, capsys):
+    """The parent relays rank 0's JSON line to stdout (anything else the
+    ranks print goes to stderr) and returns the child's exit code."""
+    prog = ("import sys; print('banner'); print('{\"metric\": \"m\", \"n_gpus\": 2}'); "
+            "sys.stdout.flush(); sys.exit(%d)")
+    monkeypatch.setattr(bench, "launch_command", lambda g, a, p: [sys.executable, "-c", prog % 0])
+    assert bench.self_launch(2, []) == 0
+    out = capsys.readouterr()
+    assert out.out.strip() == '{"metric": "m", "n_gpus": 2}'
+    assert "banner" in out.err
+    monkeypatch.setattr(bench, "launch_command", lambda g, a, p: [sys.executable, "-c", prog % 3])
+    assert bench.self_launch(2, []) == 3
+    monkeypatch.setattr(bench, "launch_command", lambda g, a, p: [sys.executable, "-c", "print('x')"])
+    assert bench.self_launch(2, []) == 1  # exit 0 but no JSON line

@@ -265,3 +265,119 @@ def test_lease_pool_bound():
     with ThreadPoolExecutor(6) as ex:
         assert all(ex.map(run, range(6)))
     f.close()
+
+
+def _erase(data, parity, er, k, m, S, stripes):
+    data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+    parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+
+
+def test_failed_pattern_build_rolls_back():
+    """a build that fails after a call created patterns
+    must not leave them in the cache.  RSMI_TEST_FAIL_FLUSH=1 makes the
+    context's first build fail (RS_ENOMEM, as an allocation failure would);
+    the call reports it and the cache is empty again.  The same patterns
+    then reconstruct exactly -- through the exclusive path (which rebuilds
+    them) and through a second call that only finds them (shared path)."""
+    k, n, S, stripes = 64, 80, 4096, 12
+    m = n - k
+    f = _fec_env(k, n, RSMI_TEST_FAIL_FLUSH="1")
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(data.data_ptr(), data.numel(), 91)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    d0, p0 = data.clone(), parity.clone()
+    rng = np.random.default_rng(91)
+    er = np.zeros((stripes, n), dtype=np.uint8)
+    for s in range(stripes):
+        er[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 1
+    _erase(data, parity, er, k, m, S, stripes)
+    with pytest.raises(rsmi.RSError) as ei:
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+    assert ei.value.code == rsmi.RS_ENOMEM
+    assert f.pattern_count() == 0  # rolled back, nothing half-built stays findable
+    for _ in range(2):  # 1st: patterns created and built again; 2nd: found (shared path)
+        data.copy_(d0)
+        parity.copy_(p0)
+        _erase(data, parity, er, k, m, S, stripes)
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+        f.sync()
+        assert torch.equal(data, d0) and torch.equal(parity, p0)
+    assert f.pattern_count() == len({row.tobytes() for row in er})
+    f.close()
+
+
+def test_eviction_counts_distinct_new_patterns():
+    """near the cap, a batch whose many stripes share ONE
+    new pattern must not evict the cache (the check counts distinct new
+    patterns, not stripes)."""
+    k, n, S, stripes = 10, 14, 4096, 64
+    m = n - k
+    f = _fec_env(k, n, RSMI_PATTERN_CAP="8")
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(data.data_ptr(), data.numel(), 5)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    d0, p0 = data.clone(), parity.clone()
+    for ids in ([0], [1], [2], [0, 1], [2, 3], [12]):  # 6 cached patterns, cap 8
+        er = np.zeros((stripes, n), dtype=np.uint8)
+        er[:, ids] = 1
+        data.copy_(d0)
+        parity.copy_(p0)
+        _erase(data, parity, er, k, m, S, stripes)
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+        f.sync()
+        assert torch.equal(data, d0) and torch.equal(parity, p0), ids
+    assert f.pattern_count() == 6 and f.pattern_evictions() == 0
+    # 64 stripes, one new pattern: 6 + 1 <= 8, no eviction
+    er = np.zeros((stripes, n), dtype=np.uint8)
+    er[:, [3, 9, 11]] = 1
+    data.copy_(d0)
+    parity.copy_(p0)
+    _erase(data, parity, er, k, m, S, stripes)
+    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+    f.sync()
+    assert torch.equal(data, d0) and torch.equal(parity, p0)
+    assert f.pattern_count() == 7 and f.pattern_evictions() == 0
+    f.close()
+
+
+def test_lease_buffers_grow_concurrently():
+    """lease buffers (device workspaces, pinned staging, the
+    host pipeline's slots) grow without a device-wide sync.  8 threads on one
+    context call DecodeBatch and Decode with monotonically growing messages,
+    so every call outgrows the buffers of the lease it gets; every result is
+    bit-exact against the oracle."""
+    k, n = 10, 14
+    f = rsmi.FEC(k, n)
+    E = oracle.fec_matrix(k, n)
+    sizes = [160 * (2 ** (i / 2)) for i in range(16)]  # 160 B .. ~29 KiB per shard
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(500 + t)
+        for i, sz in enumerate(sizes):
+            S = int(sz) + t  # ragged, distinct per thread
+            msgs = [_message(k, n, S, 10_000 * t + 100 * i + j) for j in range(1 + (i + t) % 4)]
+            batch = []
+            for data, sh in msgs:
+                keep = rng.choice(n, size=k, replace=False).tolist()
+                batch.append([rsmi.Share(x, sh[x]) for x in keep])
+            outs, st = f.DecodeBatch(batch)
+            if st != [0] * len(msgs) or any(o != d for o, (d, _) in zip(outs, msgs)):
+                errors.append(("batch", t, i))
+            data, sh = msgs[0]
+            keep = rng.choice(n, size=k, replace=False).tolist()
+            rc, ref = oracle.decode(E, k, n, [(x, sh[x]) for x in keep])
+            if rc != 0 or f.Decode(None, [rsmi.Share(x, sh[x]) for x in keep]) != ref:
+                errors.append(("decode", t, i))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    f.close()
