@@ -75,6 +75,8 @@ def parse():
                          "(H2D data, encode, D2H parity per chunk, two HIP streams); "
                          "PCIe-inclusive, never the headline")
     ap.add_argument("--stream-chunk", type=int, default=32, help="stripes per streamed chunk")
+    ap.add_argument("--chunks", type=int, default=8,
+                    help="sharded placement: exchange chunks per step (two chunks' buffers live)")
     return ap.parse_args()
 
 
@@ -550,10 +552,14 @@ def stream_main(args, world, rank, local, dev, distributed):
 def sharded_main(args, world, rank, local, dev, distributed):
     """configs[3], shard-distributed placement: shard i of every stripe is
     held by rank i mod N (the p2p analogue of main.go:207 broadcasting each
-    shard to peers).  One step = the RCCL survivor gather (one grouped
-    send/recv of exactly the survivors each owner reads, rsmi/distributed.py)
-    + rs_reconstruct_ptrs of the stripes this rank owns, reading survivors
-    where they landed.  Reported against the xGMI roofline (gathered bytes)."""
+    shard to peers).  One step = the survivor gather (exactly the survivors
+    each owner reads, rsmi/distributed.py) in --chunks chunks, chunk c + 1's
+    RCCL exchange (communication stream) overlapping chunk c's
+    rs_reconstruct_ptrs (compute stream), which reads survivors where they
+    landed.  The per-rank HBM budget is computed before anything is
+    allocated; a budget over the free HBM raises --chunks, and exits
+    non-zero with the numbers if even that cannot fit.  Reported against
+    the xGMI roofline (gathered bytes)."""
     import rsmi
     from rsmi import distributed as rd
 
@@ -565,51 +571,65 @@ def sharded_main(args, world, rank, local, dev, distributed):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     ids = rd.local_shard_ids(rank, n, world)
+    rng = np.random.default_rng(0xE4A5)  # same erasure map on every rank
+    ersets = erasure_sets(rng, args.warmup + args.steps, gstripes, n, args.emin, emax, args.pattern_pool)
+    # Plans first (host metadata, identical on every rank), then the budget.
+    free_b, _ = torch.cuda.mem_get_info(dev)
+    if os.environ.get("RSMI_BENCH_BACKEND", "nccl") != "nccl":
+        free_b //= -(-world // max(torch.cuda.device_count(), 1))  # ranks share the rehearsal GPU(s)
+    chunks = max(1, args.chunks)
+    while True:
+        tp = time.perf_counter()
+        plans = [rd.plan_exchange(er, k, n, rank, world, S, chunks=chunks) for er in ersets]
+        plan_ms = (time.perf_counter() - tp) * 1e3 / len(ersets)
+        budget = rd.hbm_budget(gstripes, len(ids), S, plans, n, k=k)
+        if budget["total"] * 1e9 <= free_b - (4 << 30) or chunks >= 64:
+            break
+        chunks *= 2
+    if budget["total"] * 1e9 > free_b - (4 << 30):
+        sys.stderr.write(f"bench.py: sharded placement needs {budget['total']:.1f} GB per rank "
+                         f"({', '.join(f'{key} {v:.1f}' for key, v in budget.items() if key != 'total')}) "
+                         f"but {free_b / 1e9:.1f} GB are free: lower --stripes\n")
+        raise SystemExit(3)
     held = torch.empty((gstripes, len(ids), S), dtype=torch.uint8, device=dev)
-    # Setup (untimed): every rank encodes the global stripes in batches and
-    # keeps its shard ids (deterministic seeds, so all ranks agree).
+    # Setup (untimed): the global data is one splitmix stream, generated in
+    # batches; a rank keeps the rows of its shard ids and encodes only when
+    # it holds parity ids (ranks holding data ids alone skip the encode).
     batch = 64
+    needs_parity = any(i >= k for i in ids)
     tmp_d = torch.empty(batch * k * S, dtype=torch.uint8, device=dev)
-    tmp_p = torch.empty(batch * m * S, dtype=torch.uint8, device=dev)
+    tmp_p = torch.empty(batch * m * S, dtype=torch.uint8, device=dev) if needs_parity else None
+    gamma = 0x9E3779B97F4A7C15
     for b0 in range(0, gstripes, batch):
         nb = min(batch, gstripes - b0)
-        f.fill_splitmix(tmp_d.data_ptr(), nb * k * S, 0x5EED + b0, sh)
-        f.encode_stripes(tmp_d.data_ptr(), k * S, tmp_p.data_ptr(), m * S, S, S, nb, sh)
-        full = torch.cat([tmp_d[:nb * k * S].view(nb, k, S), tmp_p[:nb * m * S].view(nb, m, S)], 1)
-        held[b0:b0 + nb] = full[:, ids, :]
+        f.fill_splitmix(tmp_d.data_ptr(), nb * k * S, (0x5EED + b0 * k * S // 8 * gamma) & (2**64 - 1), sh)
+        if needs_parity:
+            f.encode_stripes(tmp_d.data_ptr(), k * S, tmp_p.data_ptr(), m * S, S, S, nb, sh)
+        dv = tmp_d[:nb * k * S].view(nb, k, S)
+        for j, i in enumerate(ids):
+            held[b0:b0 + nb, j].copy_(dv[:, i] if i < k else tmp_p[:nb * m * S].view(nb, m, S)[:, i - k])
     del tmp_d, tmp_p
     if pattern_total(n, emax) <= (1 << 20):
         f.prepare_patterns(emax, sh)
-    rng = np.random.default_rng(0xE4A5)  # same erasure map on every rank
-    ersets = erasure_sets(rng, args.warmup + args.steps, gstripes, n, args.emin, emax,
-                          args.pattern_pool)
-    plans = [rd.plan_exchange(er, k, n, rank, world, S) for er in ersets]
     bufs = rd.make_buffers(plans, S, dev)
     tables = [torch.from_numpy(rd.shard_table(p, held, bufs)).to(dev) for p in plans]
+    er_owned = [np.ascontiguousarray(er[p.owned]) for er, p in zip(ersets, plans)]
     torch.cuda.synchronize(dev)
-    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    rccl = distributed and os.environ.get("RSMI_BENCH_BACKEND", "nccl") == "nccl"
+    comm = torch.cuda.Stream(dev) if rccl else None
 
-    def step(i, timed):
-        e = gev[i - args.warmup] if timed else None
-        if e:
-            e[0].record(stream)
-        rd.gather_survivors(held, plans[i], bufs)
-        if e:
-            e[1].record(stream)
-        rd.reconstruct_owned(f, plans[i], tables[i], ersets[i][plans[i].owned], S, sh)
-        if e:
-            e[2].record(stream)
+    def step(i):
+        rd.run_step(f, held, plans[i], bufs, tables[i], er_owned[i], S, stream, comm)
 
     for i in range(args.warmup):
-        step(i, False)
+        step(i)
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
-        step(i, True)
+        step(i)
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
@@ -617,9 +637,8 @@ def sharded_main(args, world, rank, local, dev, distributed):
     rec_bytes = sum(int(((k + ersets[i][plans[i].owned].sum(axis=1)) * S).sum())
                     for i in range(args.warmup, args.warmup + args.steps))
     xgmi_bytes = sum(plans[i].bytes_in for i in range(args.warmup, args.warmup + args.steps))
-    g_ms = sum(a.elapsed_time(b) for a, b, _ in gev) / args.steps
-    r_ms = sum(b.elapsed_time(c) for _, b, c in gev) / args.steps
-    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, g_ms, r_ms], dtype=torch.float64, device=stats_device(dev))
+    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, budget["total"], plan_ms], dtype=torch.float64,
+                        device=stats_device(dev))
     if distributed:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         torch.distributed.all_gather(gathered, mine)
@@ -639,14 +658,19 @@ def sharded_main(args, world, rank, local, dev, distributed):
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": f"RS({k},{n}) {args.emin}-{emax}-erasure reconstruct, shard i "
                                    f"on rank i mod N, {args.stripes} owned stripes x {S} B shards "
-                                   "per rank", "placement": "sharded"},
+                                   "per rank", "placement": "sharded", "chunks": len(plans[0].chunks),
+                       "overlap": "RCCL exchange of chunk c+1 on a communication stream || reconstruct of chunk c"
+                                  if rccl else "none (gloo rehearsal: chunks in sequence)"},
             "xgmi": {"gathered_GB": round(xgmi_total / 1e9, 3), "gathered_GB_per_step": round(xgmi_total / args.steps / 1e9, 3),
                      "achieved_GBps_total": round(xg, 1), "per_rank_GBps": round(xg / max(world, 1), 1),
                      "link_peak_GBps": 153.0, "links_per_gpu": 7},
+            "hbm_budget_GB": {key: round(v, 2) for key, v in budget.items()},
+            "hbm_free_GB": round(free_b / 1e9, 1),
+            "plan_ms_per_step": round(plan_ms, 2),
             "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),
-                          "gather_ms": round(v[3], 3), "reconstruct_ms": round(v[4], 3),
                           "gathered_GB_per_step": round(v[2] / args.steps / 1e9, 3),
-                          "reconstruct_GBps": round(v[1] / v[0] / 1e9, 2)}
+                          "reconstruct_GBps": round(v[1] / v[0] / 1e9, 2),
+                          "hbm_budget_GB": round(v[3], 2), "plan_ms": round(v[4], 2)}
                          for r, v in enumerate(per_rank)],
         })
     if distributed:

@@ -210,6 +210,22 @@ int rs_blake2b_batch(rs_ctx *ctx, int count, const uint8_t *const *msgs, const s
  * memory of count * digest_len bytes.  Enqueued on stream. */
 int rs_blake2b_device(rs_ctx *ctx, int count, const uint64_t *msg_ptrs, const uint64_t *lens,
                       const uint32_t *order, int digest_len, uint8_t *out, void *stream);
+/* rs_blake2b: the hash policy the plugin uses (hp.HashBytes, main.go:38-41,
+ * :219-223, :82-89) with a host/GPU crossover.  A single message, or a batch
+ * whose longest chain dominates, is hashed on the host CPU (C BLAKE2b, one
+ * thread per message up to the CPUs this process may use); a batch with
+ * many messages in flight goes to the GPU kernel (rs_blake2b_batch).  The
+ * choice compares the two paths' estimated times; the
+ * digests are identical either way.  RSMI_HASH=host / gpu forces a side.
+ * *where (may be NULL) reports the side taken: 0 host, 1 GPU.
+ * Replaces: hp.HashBytes(serializeMessage(...)) at main.go:219-223 (sign) and
+ * main.go:82-89 (verify). */
+int rs_blake2b(rs_ctx *ctx, int count, const uint8_t *const *msgs, const size_t *lens, int digest_len,
+               uint8_t *out, int *where);
+/* rs_blake2b_host: host-only BLAKE2b of host messages on `threads` threads
+ * (<= 0: the CPUs this process may use).  Needs no context and no GPU. */
+int rs_blake2b_host(int count, const uint8_t *const *msgs, const size_t *lens, int digest_len, uint8_t *out,
+                    int threads);
 
 /* ---- memory helpers ------------------------------------------------------
  * Engine-pinned host memory (hipHostMalloc, mapped for the device).  The

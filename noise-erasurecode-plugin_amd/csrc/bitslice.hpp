@@ -69,6 +69,14 @@ struct BitsliceKernel {
     const char* rec_name;         // "bitslice_rec_k<k>_m<m>", or nullptr
     BitsliceRecLaunch reconstruct;  // nullptr when k > 64
     int rec_iters;                  // 8 KiB column windows per reconstruct block (gen_bitslice -I)
+    // Row-subset reconstruct variants, ascending: rec_tops[i] top parity rows
+    // (m - top .. m - 1) covered by rec_top_launch[i] (gen_bitslice -T).  A
+    // stripe may use one when every parity row its pattern uses -- Rebuild's
+    // parity survivors and the erased parity rows -- is among them.
+    int n_rec_tops;
+    int rec_tops[4];
+    BitsliceRecLaunch rec_top_launch[4];
+    const char* rec_top_names[4];
 };
 
 // Generated kernel for encode of (k, k+m), or nullptr.

@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 namespace rsmi {
@@ -30,5 +31,11 @@ struct Blake2bArgs {
 };
 
 hipError_t launch_blake2b(const Blake2bArgs& a, hipStream_t stream);
+
+// Host BLAKE2b (blake2b_host.cpp): one message, and a batch spread over
+// `threads` threads (longest messages first).
+void blake2b_host(const uint8_t* msg, size_t len, int digest_len, uint8_t* out);
+void blake2b_host_batch(int count, const uint8_t* const* msgs, const size_t* lens, int digest_len, uint8_t* out,
+                        int threads);
 
 }  // namespace rsmi

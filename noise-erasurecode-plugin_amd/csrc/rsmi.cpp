@@ -7,8 +7,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <thread>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -271,6 +276,8 @@ struct rs_ctx {
     mutable std::shared_mutex pat_mu;
     rsmi::PatIndex pat_index;
     std::vector<uint32_t> h_cnt;  // [npat] erased count of each pattern
+    std::vector<uint8_t> h_lo;    // [npat] lowest parity row the pattern uses (m: none)
+    int n_tops = 0;               // row-subset syndrome kernels in use (RSMI_BITSLICE_TOPS=0: none)
     std::vector<PatKey> h_key;    // keys of the patterns created since the last flush
     GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat, d_pkey;
     size_t uploaded = 0;    // patterns built on the device
@@ -460,9 +467,30 @@ bool pick_bitslice_rec(const rsmi::BitsliceKernel* b) {
 // derived from the key on the GPU when the pattern is built
 // (invert_patterns_kernel), so a fresh pattern costs the host one index
 // insert and 32 bytes of upload.
+// Lowest parity row a pattern uses (m if none): its erased parity rows
+// (outputs) and Rebuild's parity survivors, which fill the d erased data
+// slots from the top: the d highest-numbered present parity rows.  Decides
+// which row-subset syndrome kernel covers the pattern.
+int lowest_parity_row(const PatKey& key, int k, int n) {
+    const int m = n - k;
+    int d = 0;
+    for (int i = 0; i < k; ++i) d += key.has(i);
+    int lo = m;
+    for (int t = m - 1; t >= 0; --t) {
+        if (key.has(k + t)) {
+            lo = t;  // erased parity row: an output
+        } else if (d > 0) {
+            lo = t;  // parity survivor filling an erased data slot
+            --d;
+        }
+    }
+    return lo;
+}
+
 int create_pattern(rs_ctx* c, const PatKey& key, int e) {
     const int id = static_cast<int>(c->h_cnt.size());
     c->h_cnt.push_back(static_cast<uint32_t>(e));
+    c->h_lo.push_back(static_cast<uint8_t>(lowest_parity_row(key, c->k, c->n)));
     c->h_key.push_back(key);
     c->pat_index.insert(key, id);
     return id;
@@ -535,6 +563,7 @@ void evict_patterns(rs_ctx* c) {
     c->pat_index.clear();
     c->h_key.clear();
     c->h_cnt.clear();
+    c->h_lo.clear();
     c->uploaded = 0;
     ++c->evictions;
 }
@@ -546,6 +575,7 @@ void rollback_patterns(rs_ctx* c) {
     if (c->h_cnt.size() == c->uploaded) return;
     c->pat_index.drop_from(static_cast<int>(c->uploaded));
     c->h_cnt.resize(c->uploaded);
+    c->h_lo.resize(c->uploaded);
     c->h_key.clear();
 }
 
@@ -650,29 +680,40 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     int max_e = 0;
     for (size_t i = 0; i < stripes; ++i) max_e = std::max<int>(max_e, static_cast<int>(c->h_cnt[pid[i]]));
     if (max_e == 0) return RS_OK;  // nothing erased anywhere
-    // Split between the kernels: with a bit-sliced reconstruct, stripes with
-    // few outputs may still go to the split-table kernel, whose cost grows
-    // with e while the syndrome network costs a whole encode
-    // (profiles/r01e_ab_minrec.log: the syndrome kernel wins from e = 1).
+    // Kernel of each stripe.  0: the split-table kernel.  With a bit-sliced
+    // reconstruct: stripes with at least split_e erasures go to the syndrome
+    // kernel (the split table's cost grows with e while the syndrome network
+    // costs a whole encode; profiles/r01e_ab_minrec.log: it wins from e = 1),
+    // 1..T to the smallest row-subset variant covering every parity row the
+    // pattern uses (bitslice.hpp rec_tops: fewer accumulators, more waves per
+    // SIMD), T + 1 to the full kernel.
     const int split_e = use_bitslice_rec(c) ? c->bitslice_rec_min_e : (c->m + 1);
-    auto high = [&](uint32_t p) { return static_cast<int>(c->h_cnt[p]) >= split_e; };
+    const int T = use_bitslice_rec(c) ? c->n_tops : 0;
+    const size_t nk = static_cast<size_t>(T) + 2;
+    auto kernel_of = [&](uint32_t p) -> size_t {
+        if (static_cast<int>(c->h_cnt[p]) < split_e) return 0;
+        const int lo = c->h_lo[p];
+        for (int v = 0; v < T; ++v)
+            if (c->m - c->bitslice->rec_tops[v] <= lo) return static_cast<size_t>(v) + 1;
+        return static_cast<size_t>(T) + 1;
+    };
     // Sort of the stripes by (kernel, pattern): each launch lists its
     // stripes grouped by pattern (see rs_kernels.hpp stripe_desc).  The
     // RSMI_NO_SORT knob keeps address order within a kernel (A/B runs).
     static const bool no_sort = std::getenv("RSMI_NO_SORT") != nullptr;
     const size_t npat = no_sort ? 1 : c->h_cnt.size();
-    const size_t nb = 2 * npat;
-    auto bucket = [&](size_t i) -> size_t { return (high(pid[i]) ? npat : 0) + (no_sort ? 0 : pid[i]); };
+    const size_t nb = nk * npat;
+    auto bucket = [&](size_t i) -> size_t { return kernel_of(pid[i]) * npat + (no_sort ? 0 : pid[i]); };
+    size_t count[8] = {};  // stripes per kernel (nk <= 6)
     int max_lo = 0;
-    size_t used = 0, n_lo = 0;
+    size_t used = 0;
     for (size_t i = 0; i < stripes; ++i) {
         const uint32_t p = pid[i];
         if (!c->h_cnt[p]) continue;  // stripes with nothing erased are skipped
         ++used;
-        if (!high(p)) {
-            ++n_lo;
-            max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
-        }
+        const size_t kk = kernel_of(p);
+        ++count[kk];
+        if (kk == 0) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
     }
     if (!L.st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
     uint2* desc = static_cast<uint2*>(L.st_stripe.p);
@@ -716,17 +757,19 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     L.st_stripe.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
     const uint2* d_desc = static_cast<const uint2*>(L.d_stripe_pat.p);
-    if (n_lo > 0) {
-        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, n_lo);
+    if (count[0] > 0) {
+        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, count[0]);
         set_cache_patterns(c, a);
         a.stripe_desc = d_desc;
         a.shard_ptrs = shard_ptrs;
         e = rsmi::launch_matmul(a, max_lo, s);
     }
-    if (e == hipSuccess && used > n_lo) {
+    size_t first = count[0];
+    for (size_t kk = 1; kk < nk && e == hipSuccess; first += count[kk], ++kk) {
+        if (!count[kk]) continue;
         // Generated bit-sliced reconstruct (syndromes through the fixed
         // encode network, bitslice.hpp): same descriptors and pattern cache.
-        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, used - n_lo);
+        rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, count[kk]);
         set_cache_patterns(c, a);
         rsmi::BitsliceRecArgs b{};
         b.data = a.data;
@@ -735,7 +778,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.parity_ss = a.parity_ss;
         b.pitch = a.pitch;
         b.count = a.stripes;
-        b.stripe_desc = d_desc + n_lo;
+        b.stripe_desc = d_desc + first;
         b.coef = a.coef;
         b.src = a.src;
         b.dst = a.dst;
@@ -747,7 +790,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.zpage = dev_zpage(c);
         b.shard_ptrs = shard_ptrs;
         b.xcd = c->xcd;
-        e = c->bitslice->reconstruct(b, s);
+        e = kk <= static_cast<size_t>(T) ? c->bitslice->rec_top_launch[kk - 1](b, s) : c->bitslice->reconstruct(b, s);
     }
     L.end(s);  // under pat_mu: an eviction waits for these launches
     return hip_status(e);
@@ -995,6 +1038,54 @@ int pattern_status(rs_ctx* c, size_t first, size_t count, hipStream_t s) {
     return RS_OK;
 }
 
+// CPUs this process may use: the affinity mask, then the cgroup v2 quota
+// (a GPU box gives a job a share of a large host), at least 1.
+int usable_cpus() {
+    static const int n = [] {
+        int cpus = static_cast<int>(std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
+        if (FILE* fh = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {};
+            long period = 0;
+            if (std::fscanf(fh, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+                cpus = std::min<int>(cpus, std::max<long>(1, std::atol(q) / period));
+            std::fclose(fh);
+        }
+        return std::max(1, cpus);
+    }();
+    return n;
+}
+
+// Host/GPU crossover of the hash policy (rs_blake2b).  BLAKE2b's blocks
+// chain, so the GPU kernel's time is one launch plus the longest message's
+// chain (~1.7 us per 128-byte block on 4 lanes, profiles/r02c) plus the
+// staging copy and its VALU-bound aggregate rate, while the host runs a
+// message per thread at ~0.9 GB/s (profiles/r03b).  Host when its estimate
+// is no larger.  RSMI_HASH=host / gpu forces a side; RSMI_HASH_HOST_GBPS
+// overrides the per-thread host rate.
+bool hash_on_host(int count, const size_t* lens, int threads) {
+    static const int forced = [] {
+        const char* v = std::getenv("RSMI_HASH");
+        if (!v) return 0;
+        return std::strcmp(v, "host") == 0 ? 1 : std::strcmp(v, "gpu") == 0 ? 2 : 0;
+    }();
+    if (forced) return forced == 1;
+    static const double host_bps = [] {
+        const char* v = std::getenv("RSMI_HASH_HOST_GBPS");
+        return (v ? std::max(0.01, std::atof(v)) : 0.9) * 1e9;
+    }();
+    double total = 0, longest = 0;
+    for (int i = 0; i < count; ++i) {
+        total += static_cast<double>(lens[i]);
+        longest = std::max(longest, static_cast<double>(lens[i]));
+    }
+    const double chain_blocks = std::ceil(std::max(longest, 1.0) / 128.0);
+    const double gpu_s = 80e-6 + chain_blocks * 1.7e-6 + total / 25e9 + total / 1.0e12;
+    const double host_s = std::max(longest / host_bps, total / (host_bps * threads)) + (threads > 1 ? 20e-6 * threads : 0);
+    return host_s <= gpu_s;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1038,6 +1129,11 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     c->enc = rsmi::systematic_matrix(k, n);
     c->bitslice = pick_bitslice(c->enc, k, c->m);
     c->bitslice_rec = pick_bitslice_rec(c->bitslice);
+    if (c->bitslice_rec) {
+        // Row-subset syndrome kernels (RSMI_BITSLICE_TOPS=0 keeps the full one, A/B runs).
+        const char* tv = std::getenv("RSMI_BITSLICE_TOPS");
+        c->n_tops = (tv && std::atoi(tv) == 0) ? 0 : c->bitslice->n_rec_tops;
+    }
     {
         // RS(64,16): with the network restricted to the rows a pattern uses,
         // the syndrome kernel beats the split-table kernel from e = 1
@@ -1050,6 +1146,8 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
                               ? std::string(c->bitslice->rec_name)
                               : std::string(rsmi::variant_name(k, std::min(c->m, c->bitslice_rec_min_e - 1))) + " (e<" +
                                     std::to_string(c->bitslice_rec_min_e) + ") + " + c->bitslice->rec_name;
+        for (int v = 0; v < c->n_tops; ++v)
+            c->rec_name += std::string(v ? "," : " +t") + std::to_string(c->bitslice->rec_tops[v]);
     }
     {
         // XCD-aware block order (xcd.hpp) for the bit-sliced encode and both
@@ -1675,6 +1773,29 @@ int rs_blake2b_batch(rs_ctx* c, int count, const uint8_t* const* msgs, const siz
     L.st_batch.release_after(s);
     L.st_pieces.release_after(s);
     return rc;
+}
+
+int rs_blake2b_host(int count, const uint8_t* const* msgs, const size_t* lens, int digest_len, uint8_t* out,
+                    int threads) {
+    if (count < 0 || digest_len < 1 || digest_len > 64) return RS_EINVAL;
+    if (count == 0) return RS_OK;
+    if (!msgs || !lens || !out) return RS_EINVAL;
+    for (int i = 0; i < count; ++i)
+        if (!msgs[i] && lens[i]) return RS_EINVAL;
+    rsmi::blake2b_host_batch(count, msgs, lens, digest_len, out, threads > 0 ? threads : usable_cpus());
+    return RS_OK;
+}
+
+int rs_blake2b(rs_ctx* c, int count, const uint8_t* const* msgs, const size_t* lens, int digest_len, uint8_t* out,
+               int* where) {
+    if (!c || count < 0 || digest_len < 1 || digest_len > 64) return RS_EINVAL;
+    if (where) *where = 0;
+    if (count == 0) return RS_OK;
+    if (!msgs || !lens || !out) return RS_EINVAL;
+    const int threads = std::min(count, usable_cpus());
+    if (hash_on_host(count, lens, threads)) return rs_blake2b_host(count, msgs, lens, digest_len, out, threads);
+    if (where) *where = 1;
+    return rs_blake2b_batch(c, count, msgs, lens, digest_len, out);
 }
 
 int rs_device_alloc(rs_ctx* c, size_t bytes, void** out) {

@@ -301,9 +301,12 @@ func (a *Arena) UnmarshalShard(wire []byte) (sig []byte, s Share, total, need ui
 	return sig, s, uint64(v.total_shards), uint64(v.minimum_needed_shards), nil
 }
 
-// HashBytes is the blake2b hash policy (main.go:38-41) for many messages in
-// one GPU launch (rs_blake2b_batch): digestLen bytes each (noise's policy:
-// 32).  Sign / Verify then run on the digests (main.go:219-223, :82-89).
+// HashBytes is the blake2b hash policy (main.go:38-41) for one or many
+// messages through the engine's host/GPU crossover (rs_blake2b): a single
+// message or a batch whose longest chain dominates is hashed on the host
+// CPU, many messages in one GPU launch.  digestLen bytes each (noise's
+// policy: 32).  Sign / Verify then run on the digests (main.go:219-223,
+// :82-89).
 func (f *FEC) HashBytes(msgs [][]byte, digestLen int) ([][]byte, error) {
 	n := len(msgs)
 	if n == 0 {
@@ -324,8 +327,8 @@ func (f *FEC) HashBytes(msgs [][]byte, digestLen int) ([][]byte, error) {
 		}
 	}
 	out := make([]byte, n*digestLen)
-	if st := C.rs_blake2b_batch(f.ctx, C.int(n), (**C.uint8_t)(unsafe.Pointer(&ptrs[0])), &lens[0], C.int(digestLen),
-		(*C.uint8_t)(unsafe.Pointer(&out[0]))); st != C.RS_OK {
+	if st := C.rs_blake2b(f.ctx, C.int(n), (**C.uint8_t)(unsafe.Pointer(&ptrs[0])), &lens[0], C.int(digestLen),
+		(*C.uint8_t)(unsafe.Pointer(&out[0])), nil); st != C.RS_OK {
 		return nil, statusErr(st)
 	}
 	res := make([][]byte, n)

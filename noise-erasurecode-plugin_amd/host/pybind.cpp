@@ -196,14 +196,19 @@ PYBIND11_MODULE(_rsmi_host, m) {
     m.def("NewShardPlugin",
           [](std::function<py::bytes(py::bytes)> sign, std::function<bool(py::bytes, py::bytes)> verify,
              int k, int n, int hash_len) {
-              Signer s = [sign](const std::vector<uint8_t>& msg) {
-                  py::gil_scoped_acquire g;
-                  return to_vec(sign(to_bytes(msg)));
-              };
-              Verifier v = [verify](const std::vector<uint8_t>& msg, const std::vector<uint8_t>& sig) {
-                  py::gil_scoped_acquire g;
-                  return verify(to_bytes(msg), to_bytes(sig));
-              };
+              // None -> no signing / no verification (the callbacks stay empty)
+              Signer s;
+              Verifier v;
+              if (sign)
+                  s = [sign](const std::vector<uint8_t>& msg) {
+                      py::gil_scoped_acquire g;
+                      return to_vec(sign(to_bytes(msg)));
+                  };
+              if (verify)
+                  v = [verify](const std::vector<uint8_t>& msg, const std::vector<uint8_t>& sig) {
+                      py::gil_scoped_acquire g;
+                      return verify(to_bytes(msg), to_bytes(sig));
+                  };
               return NewShardPlugin(s, v, k, n, hash_len).release();
           },
           py::arg("sign"), py::arg("verify"), py::arg("k"), py::arg("n"), py::arg("hash_len") = 0,

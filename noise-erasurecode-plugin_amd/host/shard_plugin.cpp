@@ -2,6 +2,7 @@
 #include "shard_plugin.hpp"
 
 #include <algorithm>
+#include <future>
 #include <map>
 #include <tuple>
 
@@ -122,8 +123,10 @@ Status ShardPlugin::HashBytes(const std::vector<std::vector<uint8_t>>& msgs,
         lens[i] = msgs[i].size();
     }
     std::vector<uint8_t> dig(msgs.size() * static_cast<size_t>(HashLen));
-    const int rc = rs_blake2b_batch(f->ctx(), static_cast<int>(msgs.size()), ptrs.data(), lens.data(), HashLen,
-                                    dig.data());
+    // The engine's policy: host CPU for one message or a batch whose longest
+    // chain dominates, the GPU kernel for many messages in flight.
+    const int rc = rs_blake2b(f->ctx(), static_cast<int>(msgs.size()), ptrs.data(), lens.data(), HashLen,
+                              dig.data(), nullptr);
     if (rc != RS_OK) return Status::Err(rc, std::string("blake2b: ") + rs_strerror(rc));
     for (size_t i = 0; i < msgs.size(); ++i)
         std::copy(dig.begin() + i * HashLen, dig.begin() + (i + 1) * HashLen, (*out)[i].begin());
@@ -152,15 +155,21 @@ Status ShardPlugin::shardInput(const std::vector<uint8_t>& input, std::vector<Sh
 Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
                                   std::vector<Shard>* out) {
     if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
+    // The signature hash (main.go:219-223) and the encode (main.go:225) are
+    // independent: the hash runs on this thread (host CPU, one message)
+    // while a helper thread drives the GPU encode, so the call costs about
+    // the longer of the two instead of their sum.
+    std::vector<Share> shares;
+    std::future<Status> enc = std::async(std::launch::async, [&] { return shardInput(*input, &shares); });
     std::vector<uint8_t> sig;
+    Status hs = Status::Ok();
     if (sign_) {
         std::vector<std::vector<uint8_t>> h;
-        Status hs = HashBytes({serializeMessage(self, *input)}, &h);
-        if (!hs.ok()) return hs;
-        sig = sign_(h[0]);
+        hs = HashBytes({serializeMessage(self, *input)}, &h);
+        if (hs.ok()) sig = sign_(h[0]);
     }
-    std::vector<Share> shares;
-    Status st = shardInput(*input, &shares);
+    Status st = enc.get();
+    if (!hs.ok()) return hs;
     if (!st.ok()) return st;
     out->clear();
     for (Share& s : shares) {

@@ -12,11 +12,14 @@
 // Networking, ed25519 signing and discovery are out of scope:
 // the signature scheme is a caller-supplied callback and "broadcast" is a
 // callback receiving each Shard.  The hash policy (blake2b, main.go:38-41)
-// runs on the GPU when HashLen > 0: noise's Sign(sp, hp, msg) is
+// applies when HashLen > 0: noise's Sign(sp, hp, msg) is
 // sp.Sign(hp.HashBytes(msg)), so the callbacks then receive the BLAKE2b
-// digest of serializeMessage(...) instead of the message itself, and
-// ReceiveBatch / prepareShardsBatch hash a whole batch in one launch
-// (rs_blake2b_batch).
+// digest of serializeMessage(...) instead of the message itself.  Hashing
+// goes through the engine's host/GPU crossover (rs_blake2b): the
+// single-message paths (prepareShards, Receive) hash on the host CPU --
+// prepareShards overlapping the GPU encode -- and ReceiveBatch /
+// prepareShardsBatch hash a whole batch in one GPU launch when it holds
+// enough messages.
 #pragma once
 
 #include <functional>
@@ -81,7 +84,7 @@ public:
     int TotalShards;
 
     // 0: sign/verify callbacks see the serialized message (no hash policy);
-    // 1..64: they see its BLAKE2b digest of that many bytes, hashed on the GPU.
+    // 1..64: they see its BLAKE2b digest of that many bytes (rs_blake2b policy).
     int HashLen = 0;
 
     ShardPlugin(int minimumNeededShards, int totalShards, Signer sign, Verifier verify, int hashLen = 0);
@@ -109,8 +112,8 @@ public:
     // main.go:211-241 (input == nullptr -> "network: input is null").
     Status prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
                          std::vector<Shard>* out);
-    // prepareShards for many inputs: every input's signature hash in one GPU
-    // launch (HashLen > 0), then shardInput per input.  (*out)[i] / (*sts)[i]
+    // prepareShards for many inputs: every input's signature hash in one
+    // rs_blake2b call (HashLen > 0), then shardInput per input.  (*out)[i] / (*sts)[i]
     // correspond to inputs[i].
     void prepareShardsBatch(const PeerID& self, const std::vector<std::vector<uint8_t>>& inputs,
                             std::vector<std::vector<Shard>>* out, std::vector<Status>* sts);
@@ -119,7 +122,7 @@ public:
 
     size_t PoolSize(const std::vector<uint8_t>& fileSignature) const;
 
-    // hp.HashBytes over many messages (BLAKE2b, HashLen bytes, one GPU launch);
+    // hp.HashBytes over many messages (BLAKE2b, HashLen bytes, rs_blake2b);
     // with HashLen == 0 the messages are returned unchanged.
     Status HashBytes(const std::vector<std::vector<uint8_t>>& msgs, std::vector<std::vector<uint8_t>>* out) const;
 
@@ -131,7 +134,7 @@ private:
 };
 
 // NewShardPlugin(signaturePolicy, hashPolicy, k, n)  main.go:108-115;
-// hashLen > 0 selects the GPU BLAKE2b hash policy.
+// hashLen > 0 selects the BLAKE2b hash policy.
 std::unique_ptr<ShardPlugin> NewShardPlugin(Signer sign, Verifier verify, int minimumNeededShards,
                                             int totalShards, int hashLen = 0);
 

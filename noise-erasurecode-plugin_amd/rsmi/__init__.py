@@ -42,7 +42,7 @@ EXPORTS = (
     "rs_pattern_rows",
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
     "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
-    "rs_blake2b_batch", "rs_blake2b_device",
+    "rs_blake2b_batch", "rs_blake2b_device", "rs_blake2b", "rs_blake2b_host",
     "rs_stat", "rs_arena_new", "rs_arena_alloc", "rs_arena_reset", "rs_arena_used", "rs_arena_free",
 )
 
@@ -109,6 +109,8 @@ def _lib() -> ctypes.CDLL:
             "rs_shard_unmarshal_arena": (i32, [vp, sz, vp, vp]),
             "rs_blake2b_batch": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp]),
             "rs_blake2b_device": (i32, [vp, i32, vp, vp, vp, i32, vp, vp]),
+            "rs_blake2b": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp, ctypes.POINTER(i32)]),
+            "rs_blake2b_host": (i32, [i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp, i32]),
         }
         for name, (res, args) in sig.items():
             if os.environ.get("RSMI_LIB") and not hasattr(lib, name):
@@ -331,30 +333,26 @@ class FEC:
     # -- signature hashing (blake2b policy, main.go:38-41, :219-223, :82-89) ----
     def blake2b_batch(self, messages: Sequence[bytes], digest_len: int = 32) -> List[bytes]:
         """BLAKE2b digests of many host messages in one GPU launch."""
-        cnt = len(messages)
-        if cnt == 0:
+        if not messages:
             return []
-        import numpy as np
-        lens_np = np.fromiter((len(mm) for mm in messages), dtype=np.uint64, count=cnt)
-        if cnt <= 1024 or int(lens_np.sum()) > (64 << 20):
-            # few or large messages: point at each one (no Python-side copy)
-            keep = [bytes(mm) for mm in messages]
-            ptr_np = np.fromiter((ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value or 0 for b in keep),
-                                 dtype=np.uint64, count=cnt)
-        else:
-            # many small messages: one joined buffer, pointers into it
-            keep = b"".join(bytes(mm) for mm in messages)
-            base = ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p).value or 0
-            offs = np.zeros(cnt, dtype=np.uint64)
-            np.cumsum(lens_np[:-1], out=offs[1:])
-            ptr_np = (offs + np.uint64(base)).astype(np.uint64)
-        ptrs = ptr_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p))
-        lens = lens_np.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t))
-        out = ctypes.create_string_buffer(cnt * digest_len)
-        _check(_lib().rs_blake2b_batch(self._h, cnt, ptrs, lens, digest_len,
+        keep, ptrs, lens = _message_table(messages)
+        out = ctypes.create_string_buffer(len(messages) * digest_len)
+        _check(_lib().rs_blake2b_batch(self._h, len(messages), ptrs, lens, digest_len,
                                        ctypes.cast(out, ctypes.c_void_p)), "rs_blake2b_batch")
-        raw = out.raw
-        return [raw[i * digest_len:(i + 1) * digest_len] for i in range(cnt)]
+        return _split(out.raw, len(messages), digest_len)
+
+    def blake2b(self, messages: Sequence[bytes], digest_len: int = 32):
+        """The hash policy (rs_blake2b): host CPU for one message or a batch
+        whose longest chain dominates, the GPU kernel otherwise.  Returns
+        (digests, where) with where 0 = host, 1 = GPU."""
+        if not messages:
+            return [], 0
+        keep, ptrs, lens = _message_table(messages)
+        out = ctypes.create_string_buffer(len(messages) * digest_len)
+        where = ctypes.c_int(0)
+        _check(_lib().rs_blake2b(self._h, len(messages), ptrs, lens, digest_len,
+                                 ctypes.cast(out, ctypes.c_void_p), ctypes.byref(where)), "rs_blake2b")
+        return _split(out.raw, len(messages), digest_len), where.value
 
     def blake2b_device(self, count: int, ptrs_dev: int, lens_dev: int, order_dev: int,
                        digest_len: int, out_dev: int, stream: int = 0) -> None:
@@ -400,6 +398,43 @@ class Arena:
             self.free()
         except Exception:
             pass
+
+
+def _message_table(messages: Sequence[bytes]):
+    """(keep-alive, pointer array, length array) of host messages for the
+    hash entry points: one pointer per message when there are few or large
+    ones (no Python-side copy), pointers into one joined buffer otherwise."""
+    import numpy as np
+    cnt = len(messages)
+    lens_np = np.fromiter((len(mm) for mm in messages), dtype=np.uint64, count=cnt)
+    if cnt <= 1024 or int(lens_np.sum()) > (64 << 20):
+        keep = [bytes(mm) for mm in messages]
+        ptr_np = np.fromiter((ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value or 0 for b in keep),
+                             dtype=np.uint64, count=cnt)
+    else:
+        keep = b"".join(bytes(mm) for mm in messages)
+        base = ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p).value or 0
+        offs = np.zeros(cnt, dtype=np.uint64)
+        np.cumsum(lens_np[:-1], out=offs[1:])
+        ptr_np = (offs + np.uint64(base)).astype(np.uint64)
+    keep = (keep, ptr_np, lens_np)
+    return (keep, ptr_np.ctypes.data_as(ctypes.POINTER(ctypes.c_void_p)),
+            lens_np.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)))
+
+
+def _split(raw: bytes, cnt: int, digest_len: int) -> List[bytes]:
+    return [raw[i * digest_len:(i + 1) * digest_len] for i in range(cnt)]
+
+
+def blake2b_host(messages: Sequence[bytes], digest_len: int = 32, threads: int = 0) -> List[bytes]:
+    """rs_blake2b_host: BLAKE2b on the host CPU (no context, no GPU)."""
+    if not messages:
+        return []
+    keep, ptrs, lens = _message_table(messages)
+    out = ctypes.create_string_buffer(len(messages) * digest_len)
+    _check(_lib().rs_blake2b_host(len(messages), ptrs, lens, digest_len, ctypes.cast(out, ctypes.c_void_p),
+                                  threads), "rs_blake2b_host")
+    return _split(out.raw, len(messages), digest_len)
 
 
 def NewFEC(k: int, n: int) -> FEC:

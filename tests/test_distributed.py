@@ -42,51 +42,175 @@ def test_choose_survivors_matches_oracle_rule():
         assert all(surv[i] == i for i in range(K) if not er[i])
 
 
-def test_plan_covers_each_survivor_once():
+def _plan_reference(erased, k, n, rank, world, S):
+    """The round-2 loop plan (one chunk), kept as the reference of the
+    vectorised plan: per stripe, Rebuild's survivors (in id order), then
+    holder/owner bookkeeping one shard at a time."""
+    stripes = erased.shape[0]
+    nloc = len(rd.local_shard_ids(rank, n, world))
+    owned = [s for s in range(stripes) if rd.owner(s, world) == rank]
+    send = {p: [] for p in range(world) if p != rank}
+    recv_rows = {p: [] for p in range(world) if p != rank}
+    kind = np.full((len(owned), n), rd.UNUSED, dtype=np.int8)
+    row = np.zeros((len(owned), n), dtype=np.int64)
+    n_out = 0
+    opos = {s: j for j, s in enumerate(owned)}
+    for s in range(stripes):
+        o = rd.owner(s, world)
+        surv = sorted(rd.choose_survivors(erased[s], k, n))
+        if o == rank:
+            for i in range(n):
+                if erased[s, i]:
+                    kind[opos[s], i] = rd.OUTPUT
+                    row[opos[s], i] = n_out
+                    n_out += 1
+        for i in surv:
+            hd = rd.holder(i, world)
+            if hd == rank and o == rank:
+                kind[opos[s], i] = rd.LOCAL
+                row[opos[s], i] = s * nloc + i // world
+            elif hd == rank:
+                send[o].append(s * nloc + i // world)
+            elif o == rank:
+                recv_rows[hd].append((opos[s], i))
+    recv, recv_off, off = {}, {}, 0
+    for p in sorted(recv_rows):
+        recv_off[p] = off
+        for r, (j, i) in enumerate(recv_rows[p]):
+            kind[j, i] = rd.REMOTE
+            row[j, i] = off + r
+        recv[p] = len(recv_rows[p])
+        off += recv[p]
+    return owned, kind, row, send, recv, recv_off, n_out, off * S
+
+
+def test_survivor_mask_matches_rebuild_rule():
+    rng = np.random.default_rng(3)
+    for k, n in ((10, 14), (64, 80), (4, 6), (3, 3), (17, 49)):
+        er = np.zeros((400, n), dtype=np.uint8)
+        for s in range(400):
+            er[s, rng.choice(n, size=int(rng.integers(0, n - k + 1)), replace=False)] = 1
+        mask = rd.survivor_mask(er, k, n)
+        for s in range(400):
+            assert sorted(np.nonzero(mask[s])[0].tolist()) == sorted(rd.choose_survivors(er[s], k, n))
+    with pytest.raises(ValueError):
+        rd.survivor_mask(np.ones((1, N), dtype=np.uint8), K, N)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_vectorised_plan_equals_loop_plan(world):
+    """the numpy plan equals the round-2 loop plan (one
+    chunk): same owned stripes, kinds, rows, send lists, receive counts and
+    offsets, output count and gathered bytes."""
+    rng = np.random.default_rng(world)
+    er = np.zeros((211, N), dtype=np.uint8)
+    for s in range(211):
+        er[s, rng.choice(N, size=int(rng.integers(0, N - K + 1)), replace=False)] = 1
+    for rank in range(world):
+        owned, kind, row, send, recv, recv_off, n_out, bytes_in = _plan_reference(er, K, N, rank, world, S)
+        p = rd.plan_exchange(er, K, N, rank, world, S)
+        assert p.owned.tolist() == owned
+        assert np.array_equal(p.kind, kind) and np.array_equal(p.row, row)
+        assert {q: v.tolist() for q, v in p.send.items()} == send
+        assert p.recv == recv and p.recv_off == recv_off
+        assert p.n_out == n_out and p.bytes_in == bytes_in
+
+
+def test_vectorised_plan_is_fast():
+    """The config-4 plan at N = 8 (52,424 global stripes) takes well under a
+    second (the loop plan took seconds per step)."""
+    import time
+    rng = np.random.default_rng(0)
+    G = 6553 * 8
+    er = np.zeros((G, N), dtype=np.uint8)
+    e = rng.integers(1, 5, size=G)
+    pos = np.argsort(rng.random((G, N)), axis=1)
+    for t in range(4):
+        sel = e > t
+        er[np.nonzero(sel)[0], pos[sel, t]] = 1
+    t0 = time.perf_counter()
+    p = rd.plan_exchange(er, K, N, 3, 8, 1 << 20, chunks=8)
+    assert time.perf_counter() - t0 < 2.0
+    assert len(p.chunks) == 8 and p.n_out == int(er[3::8].sum())
+
+
+@pytest.mark.parametrize("world,chunks", [(1, 3), (2, 4), (3, 5), (8, 7)])
+def test_plan_covers_each_survivor_once(world, chunks):
     _, _, er = dataset()
-    for world in (1, 2, 3, 4, 8):
-        got = {}
-        for rank in range(world):
-            p = rd.plan_exchange(er, K, N, rank, world, S)
-            for j in range(len(p.owned)):
-                for i in range(N):
-                    if p.kind[j, i] in (rd.LOCAL, rd.REMOTE):
-                        got.setdefault((rank, j, i), []).append(int(p.kind[j, i]))
-            # what peers send to `rank` equals what `rank` expects from them
-            for peer in range(world):
-                if peer == rank:
-                    continue
-                q = rd.plan_exchange(er, K, N, peer, world, S)
-                assert len(q.send[rank]) == p.recv[peer]
-        want = 0
-        for s in range(STRIPES):
-            want += K
-        assert len(got) == want and all(len(v) == 1 for v in got.values())
+    got = {}
+    plans = [rd.plan_exchange(er, K, N, r, world, S, chunks=chunks) for r in range(world)]
+    for rank, p in enumerate(plans):
+        for j in range(len(p.owned)):
+            for i in range(N):
+                if p.kind[j, i] in (rd.LOCAL, rd.REMOTE):
+                    got.setdefault((rank, j, i), []).append(int(p.kind[j, i]))
+        # what peers send to `rank` equals what `rank` expects from them, chunk by chunk
+        for peer in range(world):
+            if peer == rank:
+                continue
+            for c in range(len(p.chunks)):
+                assert len(plans[peer].chunks[c].send[rank]) == p.chunks[c].recv[peer]
+        # chunks tile the owned stripes in order
+        assert [ch.lo for ch in p.chunks][0] == 0 and p.chunks[-1].hi == len(p.owned)
+        assert all(a.hi == b.lo for a, b in zip(p.chunks, p.chunks[1:]))
+    assert len(got) == STRIPES * K and all(len(v) == 1 for v in got.values())
 
 
-def _check_gathered(plan, held, bufs, full, er, E, rank):
+def test_hbm_budget_arithmetic():
+    """The per-rank budget of the shard-distributed step, before allocation:
+    holder buffer, two chunk slots of send / receive rows, the output rows,
+    tables and the setup batch; more chunks shrink only the slots."""
+    G, world, Sb = 6553 * 8, 8, 1 << 20
+    rng = np.random.default_rng(1)
+    er = np.zeros((G, N), dtype=np.uint8)
+    e = rng.integers(1, 5, size=G)
+    pos = np.argsort(rng.random((G, N)), axis=1)
+    for t in range(4):
+        sel = e > t
+        er[np.nonzero(sel)[0], pos[sel, t]] = 1
+    nloc = len(rd.local_shard_ids(0, N, world))
+    b1 = rd.hbm_budget(G, nloc, Sb, [rd.plan_exchange(er, K, N, 0, world, Sb, chunks=1)], N, k=K)
+    b8 = rd.hbm_budget(G, nloc, Sb, [rd.plan_exchange(er, K, N, 0, world, Sb, chunks=8)], N, k=K)
+    assert b1["held"] == b8["held"] == G * nloc * Sb / 1e9
+    assert abs(b1["out"] - int(er[0::8].sum()) * Sb / 1e9) < 1e-9
+    assert b8["send"] < b1["send"] / 3 and b8["recv"] < b1["recv"] / 3  # 2 slots of 1/8 vs 1 slot of all
+    assert abs(b8["total"] - sum(v for key, v in b8.items() if key != "total")) < 1e-6
+    assert b1["total"] > 200 and b8["total"] < 170  # GB: the round-2 sizing vs chunked slots
+
+
+def test_buffers_require_16_byte_rows():
+    """shard rows must stay 16-byte aligned for the kernels."""
+    _, _, er = dataset()
+    p = rd.plan_exchange(er, K, N, 0, 1, 100)
+    with pytest.raises(ValueError):
+        rd.make_buffers([p], 100, "cpu")
+
+
+def _check_gathered(plan, held, bufs, full, er, E, rank, chunk=None):
     """Every survivor Rebuild reads is where the shard table says; the
     erased shards, reconstructed (by the oracle here; by rs_reconstruct_ptrs
-    on the GPU) from exactly those bytes, equal the originals."""
+    on the GPU) from exactly those bytes, equal the originals.  With `chunk`,
+    only that chunk's owned stripes (whose slot was just filled)."""
     from oracle import oracle
-    owned = plan.owned
+    lo, hi = (0, len(plan.owned)) if chunk is None else (plan.chunks[chunk].lo, plan.chunks[chunk].hi)
+    owned = list(plan.owned[lo:hi])
     data = np.zeros((len(owned), K, S), dtype=np.uint8)
     par = np.zeros((len(owned), N - K, S), dtype=np.uint8)
     for j, s in enumerate(owned):
         surv = rd.choose_survivors(er[s], K, N)
         for i in range(N):
             if i in surv:
-                got = rd.shard_bytes_at(plan, held, bufs, j, i).numpy()
+                got = rd.shard_bytes_at(plan, held, bufs, lo + j, i).numpy()
                 assert (got == full[s, i]).all(), (rank, s, i)
                 (data[j, i] if i < K else par[j, i - K])[:] = got
             else:
-                assert er[s, i] or plan.kind[j, i] == rd.UNUSED
+                assert er[s, i] or plan.kind[lo + j, i] == rd.UNUSED
                 (data[j, i] if i < K else par[j, i - K])[:] = 0xEE
     erw = np.ascontiguousarray(er[owned])
     assert oracle.reconstruct_batch(E, K, N, data, par, S, len(owned), erw) == 0
     for j, s in enumerate(owned):
         for i in np.nonzero(erw[j])[0]:
-            assert plan.kind[j, i] == rd.OUTPUT
+            assert plan.kind[lo + j, i] == rd.OUTPUT
             got = data[j, i] if i < K else par[j, i - K]
             assert (got == full[s, i]).all(), (rank, s, i)
 
@@ -99,10 +223,17 @@ def _worker(rank, world, port, q):
         E, full, er = dataset()
         ids = rd.local_shard_ids(rank, N, world)
         held = torch.from_numpy(np.ascontiguousarray(full[:, ids, :]))
-        plan = rd.plan_exchange(er, K, N, rank, world, S)
-        bufs = rd.make_buffers([plan], S, "cpu")
-        rd.gather_survivors(held, plan, bufs)
-        _check_gathered(plan, held, bufs, full, er, E, rank)
+        for chunks in (1, 3):
+            plan = rd.plan_exchange(er, K, N, rank, world, S, chunks=chunks)
+            bufs = rd.make_buffers([plan], S, "cpu")
+            if chunks == 1:
+                rd.gather_survivors(held, plan, bufs)
+                _check_gathered(plan, held, bufs, full, er, E, rank)
+                continue
+            # chunk by chunk: each chunk's survivors are in its slot right after its exchange
+            for c in range(len(plan.chunks)):
+                rd.gather_survivors(held, plan, bufs, chunk=c)
+                _check_gathered(plan, held, bufs, full, er, E, rank, chunk=c)
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok", plan.bytes_in))
@@ -173,5 +304,5 @@ def test_plan_send_recv_orders_agree():
             for r, hrow in enumerate(rows):
                 s, slot = divmod(int(hrow), nloc)
                 i = p + slot * world
-                j = po.owned.index(s)
+                j = po.owned.tolist().index(s)
                 assert po.kind[j, i] == rd.REMOTE and po.row[j, i] == po.recv_off[p] + r

@@ -125,3 +125,28 @@ def test_blake2b_bad_arguments():
         assert lib.rs_blake2b_batch(fec().handle, 1, ptrs, lens, dl, ctypes.cast(out, ctypes.c_void_p)) == rsmi.RS_EINVAL
     lens[0] = 5  # NULL message with a length
     assert lib.rs_blake2b_batch(fec().handle, 1, ptrs, lens, 32, ctypes.cast(out, ctypes.c_void_p)) == rsmi.RS_EINVAL
+
+
+def test_hash_policy_crossover_bit_exact():
+    """rs_blake2b: one message -- or a few long ones -- is
+    hashed on the host, many short ones on the GPU; the digests equal
+    hashlib's on both sides of the crossover, for 32- and 64-byte digests."""
+    f = fec()
+    rng = np.random.default_rng(3)
+    cases = [
+        ([_msg(1048580 + 40, 1)], 0),                                    # config-1 message: host
+        ([_msg(65536, 10 + i) for i in range(4)], 0),                     # 4 long chains: host
+        ([_msg(int(rng.integers(0, 2048)), 100 + i) for i in range(8192)], 1),  # many short: GPU
+    ]
+    for msgs, want_where in cases:
+        for dl in (32, 64):
+            got, where = f.blake2b(msgs, dl)
+            assert where == want_where, (len(msgs), dl)
+            assert got == [hashlib.blake2b(m, digest_size=dl).digest() for m in msgs]
+
+
+def test_host_and_gpu_sides_agree_on_edges():
+    msgs = [_msg(n, 7 + n) for n in EDGE]
+    f = fec()
+    for dl in (1, 32, 64):
+        assert rsmi.blake2b_host(msgs, dl) == f.blake2b_batch(msgs, dl)

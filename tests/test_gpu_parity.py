@@ -249,9 +249,10 @@ def _fec_env(k, n, **env):
 def test_bitslice_reconstruct_kernel_selection():
     """Batched reconstruct of a bit-sliced code goes through the generated
     syndrome kernel (bitslice.hpp) unless RSMI_BITSLICE_REC=0."""
-    assert fec(64, 80).kernel_name(1) == "bitslice_rec_k64_m16"
+    assert fec(64, 80).kernel_name(1) == "bitslice_rec_k64_m16 +t4,8"
+    assert _fec_env(64, 80, RSMI_BITSLICE_TOPS="0").kernel_name(1) == "bitslice_rec_k64_m16"
     assert _fec_env(64, 80, RSMI_BITSLICE_REC_MIN_E="5").kernel_name(1) == \
-        "K64_MG4_B256 (e<5) + bitslice_rec_k64_m16"
+        "K64_MG4_B256 (e<5) + bitslice_rec_k64_m16 +t4,8"
     assert _fec_env(64, 80, RSMI_BITSLICE_REC="0").kernel_name(1).startswith("K64_MG16")
     assert fec(10, 14).kernel_name(1).startswith("K10_MG4")
     assert _fec_env(10, 14, RSMI_BITSLICE="1", RSMI_BITSLICE_REC_MIN_E="1").kernel_name(1) == \
@@ -305,6 +306,85 @@ def test_bitslice_reconstruct_roundtrip(k, n, S, pitch):
         assert torch.equal(pv[:, :, :S], pv0[:, :, :S]), f.kernel_name(1)
     fb.close()
     ft.close()
+
+
+def _lowest_parity_row(er_row, k, n):
+    """Python restatement of rsmi.cpp lowest_parity_row: the lowest parity
+    row a pattern uses (erased parity outputs and Rebuild's parity
+    survivors), m if none."""
+    from rsmi import distributed as rd
+    m = n - k
+    used = [t for t in range(m) if er_row[k + t]]
+    used += [i - k for i in rd.choose_survivors(er_row, k, n) if i >= k]
+    return min(used) if used else m
+
+
+@pytest.mark.parametrize("S,pitch", [(8192, 8192), (1000, 1008), (65536 + 16, 65536 + 16)])
+def test_row_subset_syndrome_kernels(S, pitch):
+    """RS(64,16) stripes whose patterns use only the top 4 or
+    top 8 parity rows go to the row-subset syndrome kernels (t4: 127 VGPRs,
+    t8: 132, vs 199 for all 16 rows).  Edge patterns on both sides of each
+    boundary plus random ones, in one call (several launches); the result
+    equals the originals and the full kernel's (RSMI_BITSLICE_TOPS=0)."""
+    k, n = 64, 80
+    m = n - k
+    pats = [
+        [0], [63], [0, 1, 2, 3], [60, 61, 62, 63], [k + 15], [k + 12], [k + 12, 0, 1, 2],  # top 4
+        [0, 1, 2, 3, 4], [k + 11], [k + 8, 5], list(range(8)), [k + 12, k + 13, 0, 1, 2, 3, 4, 5],  # top 8
+        list(range(9)), [k + 7], [k + 0, 1], list(range(16)), list(range(k, n)),  # full
+        [k + 15, k + 14, k + 13, k + 12, 0],  # 4 top rows erased + 1 data: survivor row 11 -> t8
+    ]
+    er = np.zeros((len(pats), n), dtype=np.uint8)
+    for r, pl in enumerate(pats):
+        er[r, pl] = 1
+    rng = np.random.default_rng(S)
+    er = np.concatenate([er, _erasures(rng, 40, n, m)])
+    lows = [_lowest_parity_row(row, k, n) for row in er]
+    assert {0, 1, 2} <= {0 if lo >= 12 else 1 if lo >= 8 else 2 for lo in lows}  # all three kernels used
+    stripes = len(er)
+    f_top = fec(64, 80)
+    f_full = _fec_env(64, 80, RSMI_BITSLICE_TOPS="0")
+    data, parity = _dev_stripes(f_top, stripes, S, pitch, 5 + S)
+    f_top.encode_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes)
+    f_top.sync()
+    d0, p0 = data.clone(), parity.clone()
+    for f in (f_top, f_full):
+        data.copy_(d0)
+        parity.copy_(p0)
+        dv, pv = data.view(stripes, k, pitch), parity.view(stripes, m, pitch)
+        dv[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0xA5
+        pv[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0x5A
+        f.reconstruct_stripes(data.data_ptr(), k * pitch, parity.data_ptr(), m * pitch, pitch, S, stripes,
+                              er.tobytes())
+        f.sync()
+        dv0, pv0 = d0.view(stripes, k, pitch), p0.view(stripes, m, pitch)
+        assert torch.equal(dv[:, :, :S], dv0[:, :, :S]), f.kernel_name(1)
+        assert torch.equal(pv[:, :, :S], pv0[:, :, :S]), f.kernel_name(1)
+    # and in pointer mode, every shard at a random row of a pool
+    _check_ptrs_roundtrip(f_top, k, n, S, er, 77 + S)
+    f_full.close()
+
+
+def _check_ptrs_roundtrip(f, k, n, S, er, seed):
+    stripes = len(er)
+    Sp = (S + 15) // 16 * 16  # shard addresses must be 16-byte aligned
+    pool = torch.empty((stripes * n, Sp), dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(pool.data_ptr(), pool.numel(), seed)
+    rows = torch.from_numpy(np.random.default_rng(seed).permutation(stripes * n).reshape(stripes, n)).cuda()
+    m = n - k
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(data.data_ptr(), data.numel(), seed + 1)
+    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.sync()
+    full = torch.cat([data.view(stripes, k, S), parity.view(stripes, m, S)], dim=1)
+    pool[rows.view(-1), :S] = full.reshape(-1, S)
+    erb = torch.from_numpy(er.astype(bool)).cuda()
+    pool[rows[erb]] = 0
+    table = (pool.data_ptr() + rows.to(torch.int64) * Sp).contiguous()
+    f.reconstruct_ptrs(table.data_ptr(), S, stripes, er.tobytes())
+    f.sync()
+    assert torch.equal(pool[rows.view(-1), :S].view(stripes, n, S), full)
 
 
 def test_reconstruct_split_between_kernels():
@@ -576,30 +656,38 @@ def test_distributed_gather_and_pointer_reconstruct(world):
     full = torch.cat([data.view(stripes, k, S), parity.view(stripes, n - k, S)], dim=1).contiguous()
     er = _erasures(np.random.default_rng(9 + world), stripes, n, n - k)
     held = [full[:, rd.local_shard_ids(r, n, world), :].contiguous() for r in range(world)]
-    plans = [rd.plan_exchange(er, k, n, r, world, S) for r in range(world)]
-    bufs = [rd.make_buffers([plans[r]], S, "cuda") for r in range(world)]
-    if world == 1:
-        rd.gather_survivors(held[0], plans[0], bufs[0])
-    for p in range(world):  # sender packing, as gather_survivors does it
-        flat = held[p].view(-1, S)
-        for o, rows in plans[p].send.items():
-            if len(rows):
-                seg = bufs[p].send[plans[p].send_off[o]:plans[p].send_off[o] + len(rows)]
-                torch.index_select(flat, 0, torch.from_numpy(rows).cuda(), out=seg)
-    for o in range(world):  # the transport
-        for p, cnt in plans[o].recv.items():
-            if cnt:
-                so = plans[p].send_off[o]
-                bufs[o].recv[plans[o].recv_off[p]:plans[o].recv_off[p] + cnt].copy_(bufs[p].send[so:so + cnt])
-    for o in range(world):
-        pl = plans[o]
-        bufs[o].out.fill_(0xA5)
-        table = torch.from_numpy(rd.shard_table(pl, held[o], bufs[o])).cuda()
-        rd.reconstruct_owned(f, pl, table, er[pl.owned], S)
-        f.sync()
-        for j, s in enumerate(pl.owned):
-            for i in np.nonzero(er[s])[0]:
-                assert torch.equal(bufs[o].out[int(pl.row[j, i])], full[s, i]), (world, o, s, i)
+    for chunks in (1, 3):
+        plans = [rd.plan_exchange(er, k, n, r, world, S, chunks=chunks) for r in range(world)]
+        bufs = [rd.make_buffers([plans[r]], S, "cuda") for r in range(world)]
+        if world == 1:
+            for c in range(len(plans[0].chunks)):
+                rd.gather_survivors(held[0], plans[0], bufs[0], chunk=c)
+        tables = [torch.from_numpy(rd.shard_table(plans[o], held[o], bufs[o])).cuda() for o in range(world)]
+        for o in range(world):
+            bufs[o].out.fill_(0xA5)
+        for c in range(len(plans[0].chunks)):
+            for p in range(world):  # sender packing of chunk c, as gather_survivors does it
+                flat = held[p].view(-1, S)
+                ch = plans[p].chunks[c]
+                for o, rows in ch.send.items():
+                    if len(rows):
+                        seg = bufs[p].send[c % bufs[p].slots][ch.send_off[o]:ch.send_off[o] + len(rows)]
+                        torch.index_select(flat, 0, torch.from_numpy(rows).cuda(), out=seg)
+            for o in range(world):  # the transport into o's slot
+                ch = plans[o].chunks[c]
+                for p, cnt in ch.recv.items():
+                    if cnt:
+                        so = plans[p].chunks[c].send_off[o]
+                        bufs[o].recv[c % bufs[o].slots][ch.recv_off[p]:ch.recv_off[p] + cnt].copy_(
+                            bufs[p].send[c % bufs[p].slots][so:so + cnt])
+            for o in range(world):  # chunk c's reconstruct (before its slot is reused)
+                rd.reconstruct_owned(f, plans[o], tables[o], er[plans[o].owned], S, chunk=c)
+            f.sync()
+        for o in range(world):
+            pl = plans[o]
+            for j, s in enumerate(pl.owned):
+                for i in np.nonzero(er[s])[0]:
+                    assert torch.equal(bufs[o].out[int(pl.row[j, i])], full[s, i]), (world, chunks, o, s, i)
 
 
 @pytest.mark.parametrize("k,n,S", [(10, 14, 4099), (64, 80, 8192), (4, 6, 100), (17, 49, 1000)])

@@ -371,3 +371,29 @@ def test_prepare_shards_batch_matches_single():
     for inp, shards in zip(inputs[:-1], out[:-1]):
         assert shards == p.prepareShards(SELF, inp)
     assert p.HashBytes([b"abc"]) == [hashlib.blake2b(b"abc", digest_size=32).digest()]
+
+
+def test_prepare_shards_hash_overlaps_encode():
+    """prepareShards of the config-1 blob with the hash
+    policy costs about one host hash (the GPU encode runs beside it), not a
+    GPU hash chain (~15 ms).  The bound is loose -- the shares and signature
+    are checked exactly, the time only against a clear regression."""
+    import time
+    k, n = 10, 14
+    blob = oracle.splitmix_bytes(1048580, 11).tobytes()
+    signed = []
+    p = h.NewShardPlugin(_digest_sign(signed), _digest_verify([]), k, n, hash_len=32)
+    me = h.PeerID("127.0.0.1:3000", b"me")
+    p.prepareShards(me, blob)  # warm: contexts, leases, staging
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        shards = p.prepareShards(me, blob)
+        ts.append(time.perf_counter() - t0)
+    want = hashlib.blake2b(h.serializeMessage(me, blob), digest_size=32).digest()
+    assert signed[-1] == want
+    E = oracle.fec_matrix(k, n)
+    par = oracle.encode(E, k, n, blob)
+    S = len(blob) // k
+    assert b"".join(s.ShardData for s in shards[k:]) == par
+    assert min(ts) < 0.008, ts  # host hash ~1.2-1.7 ms + encode 0.13 ms; the GPU chain alone is ~15 ms
