@@ -291,7 +291,9 @@ class FEC:
     def reconstruct_ptrs(self, shard_ptrs_dev: int, shard_len: int, stripes: int, erased: bytes,
                          stream: int = 0) -> None:
         """rs_reconstruct_ptrs: shard i of stripe s at the device address in
-        the device array shard_ptrs_dev[s * n + i]."""
+        the device array shard_ptrs_dev[s * n + i].  Every address must be
+        16-byte aligned (the kernels move 16-byte vectors; rsmi.h), e.g. rows
+        of a pool whose row pitch is a multiple of 16."""
         if len(erased) != stripes * self.n:
             raise RSError(RS_EINVAL, "erased must hold stripes*n flags")
         buf = ctypes.c_char_p(bytes(erased))

@@ -19,4 +19,5 @@ done
 timeout -k 10 240 $B --emin 16 --emax 16 > $O/e16.json 2>> $O/err.log || exit 6
 RSMI_BENCH_BACKEND=gloo timeout -k 10 600 python3 bench.py --gpus 2 --placement sharded --stripes 1500 --steps 3 --warmup 1 > $O/sharded2_gloo.json 2> $O/sharded2_gloo.err || exit 7
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 8
+timeout -k 10 300 tools/membench9 > $O/membench9.log 2>&1 || exit 9
 echo done
