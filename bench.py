@@ -637,8 +637,24 @@ def sharded_main(args, world, rank, local, dev, distributed):
     rec_bytes = sum(int(((k + ersets[i][plans[i].owned].sum(axis=1)) * S).sum())
                     for i in range(args.warmup, args.warmup + args.steps))
     xgmi_bytes = sum(plans[i].bytes_in for i in range(args.warmup, args.warmup + args.steps))
-    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, budget["total"], plan_ms], dtype=torch.float64,
-                        device=stats_device(dev))
+    # Check (untimed) the last step's outputs on a sample of owned stripes:
+    # each stripe regenerated from the global stream and encoded here, its
+    # erased shards compared with what the gather + reconstruct produced.
+    last = plans[-1]
+    sample = np.unique(np.linspace(0, len(last.owned) - 1, num=min(16, len(last.owned))).astype(np.int64))
+    chk_d = torch.empty(k * S, dtype=torch.uint8, device=dev)
+    chk_p = torch.empty(m * S, dtype=torch.uint8, device=dev)
+    bad = 0
+    for j in sample:
+        gs = int(last.owned[j])
+        f.fill_splitmix(chk_d.data_ptr(), k * S, (0x5EED + gs * k * S // 8 * gamma) & (2**64 - 1), sh)
+        f.encode_stripes(chk_d.data_ptr(), k * S, chk_p.data_ptr(), m * S, S, S, 1, sh)
+        full = torch.cat([chk_d.view(k, S), chk_p.view(m, S)])
+        for i in np.nonzero(ersets[-1][gs])[0]:
+            bad += int(not torch.equal(bufs.out[int(last.row[j, i])], full[i]))
+    torch.cuda.synchronize(dev)
+    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, budget["total"], plan_ms, len(sample), bad],
+                        dtype=torch.float64, device=stats_device(dev))
     if distributed:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
         torch.distributed.all_gather(gathered, mine)
@@ -667,6 +683,8 @@ def sharded_main(args, world, rank, local, dev, distributed):
             "hbm_budget_GB": {key: round(v, 2) for key, v in budget.items()},
             "hbm_free_GB": round(free_b / 1e9, 1),
             "plan_ms_per_step": round(plan_ms, 2),
+            "verified": {"stripes": int(sum(r[5] for r in per_rank)), "mismatched_shards": int(sum(r[6] for r in per_rank)),
+                         "how": "last step, up to 16 owned stripes per rank regenerated and encoded locally"},
             "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),
                           "gathered_GB_per_step": round(v[2] / args.steps / 1e9, 3),
                           "reconstruct_GBps": round(v[1] / v[0] / 1e9, 2),
@@ -675,6 +693,8 @@ def sharded_main(args, world, rank, local, dev, distributed):
         })
     if distributed:
         torch.distributed.destroy_process_group()
+    if sum(r[6] for r in per_rank):
+        raise SystemExit("bench.py: sharded reconstruct produced wrong shards")
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <thread>
@@ -1059,31 +1060,61 @@ int usable_cpus() {
 
 // Host/GPU crossover of the hash policy (rs_blake2b).  BLAKE2b's blocks
 // chain, so the GPU kernel's time is one launch plus the longest message's
-// chain (~1.7 us per 128-byte block on 4 lanes, profiles/r02c) plus the
-// staging copy and its VALU-bound aggregate rate, while the host runs a
-// message per thread at ~0.9 GB/s (profiles/r03b).  Host when its estimate
-// is no larger.  RSMI_HASH=host / gpu forces a side; RSMI_HASH_HOST_GBPS
-// overrides the per-thread host rate.
-bool hash_on_host(int count, const size_t* lens, int threads) {
+// chain (~1.76 us per 128-byte block on 4 lanes) plus the staging copies and
+// its VALU-bound aggregate rate, while the host runs a message per thread at
+// the rate measured once on this machine (1.73 GB/s per thread on the GPU
+// box's EPYC 9575F, profiles/r03c/hash_policy.json), each extra thread
+// costing ~25 us to start.  Both estimates are minimised over the host
+// thread count; the host wins ties.  RSMI_HASH=host / gpu forces a side;
+// RSMI_HASH_HOST_GBPS overrides the calibrated per-thread rate.
+struct HashPlan {
+    bool host;
+    int threads;
+};
+
+double host_hash_rate() {
+    static const double bps = [] {
+        if (const char* v = std::getenv("RSMI_HASH_HOST_GBPS")) return std::max(0.01, std::atof(v)) * 1e9;
+        std::vector<uint8_t> buf(size_t(128) << 10, 0x5A);
+        uint8_t d[32];
+        double best = 1e9;
+        for (int r = 0; r < 3; ++r) {
+            const auto t0 = std::chrono::steady_clock::now();
+            rsmi::blake2b_host(buf.data(), buf.size(), 32, d);
+            best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        }
+        return static_cast<double>(buf.size()) / std::max(best, 1e-6);
+    }();
+    return bps;
+}
+
+HashPlan plan_hash(int count, const size_t* lens) {
     static const int forced = [] {
         const char* v = std::getenv("RSMI_HASH");
         if (!v) return 0;
         return std::strcmp(v, "host") == 0 ? 1 : std::strcmp(v, "gpu") == 0 ? 2 : 0;
-    }();
-    if (forced) return forced == 1;
-    static const double host_bps = [] {
-        const char* v = std::getenv("RSMI_HASH_HOST_GBPS");
-        return (v ? std::max(0.01, std::atof(v)) : 0.9) * 1e9;
     }();
     double total = 0, longest = 0;
     for (int i = 0; i < count; ++i) {
         total += static_cast<double>(lens[i]);
         longest = std::max(longest, static_cast<double>(lens[i]));
     }
+    const double h = host_hash_rate();
+    constexpr double kThreadCost = 25e-6;
+    const int tmax = std::max(1, std::min(count, usable_cpus()));
+    int best_t = 1;
+    double host_s = 1e30;
+    for (int t = 1; t <= tmax; ++t) {
+        const double est = std::max(longest / h, total / (h * t)) + kThreadCost * (t - 1);
+        if (est < host_s) {
+            host_s = est;
+            best_t = t;
+        }
+    }
+    if (forced) return {forced == 1, best_t};
     const double chain_blocks = std::ceil(std::max(longest, 1.0) / 128.0);
-    const double gpu_s = 80e-6 + chain_blocks * 1.7e-6 + total / 25e9 + total / 1.0e12;
-    const double host_s = std::max(longest / host_bps, total / (host_bps * threads)) + (threads > 1 ? 20e-6 * threads : 0);
-    return host_s <= gpu_s;
+    const double gpu_s = 80e-6 + chain_blocks * 1.76e-6 + total / 50e9 + total / 1.0e12;
+    return {host_s <= gpu_s, best_t};
 }
 
 }  // namespace
@@ -1792,8 +1823,8 @@ int rs_blake2b(rs_ctx* c, int count, const uint8_t* const* msgs, const size_t* l
     if (where) *where = 0;
     if (count == 0) return RS_OK;
     if (!msgs || !lens || !out) return RS_EINVAL;
-    const int threads = std::min(count, usable_cpus());
-    if (hash_on_host(count, lens, threads)) return rs_blake2b_host(count, msgs, lens, digest_len, out, threads);
+    const HashPlan hp = plan_hash(count, lens);
+    if (hp.host) return rs_blake2b_host(count, msgs, lens, digest_len, out, hp.threads);
     if (where) *where = 1;
     return rs_blake2b_batch(c, count, msgs, lens, digest_len, out);
 }

@@ -156,21 +156,23 @@ Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>
                                   std::vector<Shard>* out) {
     if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
     // The signature hash (main.go:219-223) and the encode (main.go:225) are
-    // independent: the hash runs on this thread (host CPU, one message)
-    // while a helper thread drives the GPU encode, so the call costs about
-    // the longer of the two instead of their sum.
+    // independent: a helper thread hashes (one message: host CPU, no HIP
+    // calls) while this thread, whose HIP state is warm, drives the GPU
+    // encode, so the call costs about the longer of the two, not their sum.
+    // The signer itself runs here, after both.
     std::vector<Share> shares;
-    std::future<Status> enc = std::async(std::launch::async, [&] { return shardInput(*input, &shares); });
     std::vector<uint8_t> sig;
-    Status hs = Status::Ok();
+    std::vector<std::vector<uint8_t>> h;
+    std::future<Status> hashed;
     if (sign_) {
-        std::vector<std::vector<uint8_t>> h;
-        hs = HashBytes({serializeMessage(self, *input)}, &h);
-        if (hs.ok()) sig = sign_(h[0]);
+        std::vector<std::vector<uint8_t>> ser{serializeMessage(self, *input)};
+        hashed = std::async(std::launch::async, [this, ser = std::move(ser), &h] { return HashBytes(ser, &h); });
     }
-    Status st = enc.get();
+    Status st = shardInput(*input, &shares);
+    Status hs = sign_ ? hashed.get() : Status::Ok();
     if (!hs.ok()) return hs;
     if (!st.ok()) return st;
+    if (sign_) sig = sign_(h[0]);
     out->clear();
     for (Share& s : shares) {
         Shard m;

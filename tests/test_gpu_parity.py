@@ -372,12 +372,12 @@ def _check_ptrs_roundtrip(f, k, n, S, er, seed):
     f.fill_splitmix(pool.data_ptr(), pool.numel(), seed)
     rows = torch.from_numpy(np.random.default_rng(seed).permutation(stripes * n).reshape(stripes, n)).cuda()
     m = n - k
-    data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
-    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+    data = torch.empty(stripes * k * Sp, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(stripes * m * Sp, dtype=torch.uint8, device="cuda")
     f.fill_splitmix(data.data_ptr(), data.numel(), seed + 1)
-    f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f.encode_stripes(data.data_ptr(), k * Sp, parity.data_ptr(), m * Sp, Sp, S, stripes)
     f.sync()
-    full = torch.cat([data.view(stripes, k, S), parity.view(stripes, m, S)], dim=1)
+    full = torch.cat([data.view(stripes, k, Sp), parity.view(stripes, m, Sp)], dim=1)[:, :, :S]
     pool[rows.view(-1), :S] = full.reshape(-1, S)
     erb = torch.from_numpy(er.astype(bool)).cuda()
     pool[rows[erb]] = 0

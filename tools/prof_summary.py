@@ -147,13 +147,30 @@ def main():
         if rec:
             lines.append("")
             split = any("rs_matmul_kernel" in r["Kernel_Name"] for r in all_tr)
-            what = ("the split-table launch (stripes with e below RSMI_BITSLICE_REC_MIN_E) plus the syndrome launch"
-                    if split else "one syndrome launch (every erasure count)")
-            rms = statistics.mean((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rec)
+            variants = sorted({short_name(r["Kernel_Name"]) for r in rec})
+            what = ("the split-table launch (stripes with e below RSMI_BITSLICE_REC_MIN_E) plus the syndrome launches"
+                    if split else f"the syndrome launches ({', '.join(f'`{v}`' for v in variants)}: each stripe in "
+                                  "the smallest row-subset kernel covering its pattern)")
+            # steps = encode launches (mode both) or, in reconstruct mode, launches of the full kernel
+            steps = len(enc) if a.mode == "both" and enc else max(1, len([r for r in rec if "_t" not in short_name(r["Kernel_Name"])]))
+            rms = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rec) / steps
             alg_rec = st * (k + (m + 1) / 2) * S
+            rec_pmc = []
+            for cnt, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+                v = [float(r["Counter_Value"]) for r in rows(os.path.join(a.dir, sub, "run_counter_collection.csv"))
+                     if r["Counter_Name"] == cnt and "rs_bitslice_rec" in r["Kernel_Name"]]
+                rec_pmc.append(v)
+            tail = ""
+            if rec_pmc[0] and rec_pmc[1]:
+                # the PMC runs have their own step counts: normalise by their full-kernel launches
+                psteps = max(1, len([1 for r in rows(os.path.join(a.dir, "fetch", "run_counter_collection.csv"))
+                                     if r["Counter_Name"] == "FETCH_SIZE" and "rs_bitslice_rec" in r["Kernel_Name"]
+                                     and "_t" not in short_name(r["Kernel_Name"])]))
+                tr_gb = (sum(rec_pmc[0]) * 2 + sum(rec_pmc[1])) * 1024 / 1e9 / psteps
+                tail = f" HBM traffic {tr_gb:.2f} GB per step (FETCH x2 + WRITE over its launches)."
             lines.append(f"Reconstruct per step = {what}; expected algorithmic bytes {alg_rec / 1e9:.2f} GB "
                          f"(uniform 1..m erasures)" + ("." if split else
-                         f" / {rms:.3f} ms = **{alg_rec / (rms / 1e3) / 1e9:.0f} GB/s**."))
+                         f" / {rms:.3f} ms of kernel time per step = **{alg_rec / (rms / 1e3) / 1e9:.0f} GB/s**.") + tail)
     rl = ["Per role (launch order alternates encode / reconstruct):"]
     rl.append("")
     rl.append("| role | launches | avg ms | grid (threads) | workgroup |")
