@@ -1161,9 +1161,12 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
     c->bitslice = pick_bitslice(c->enc, k, c->m);
     c->bitslice_rec = pick_bitslice_rec(c->bitslice);
     if (c->bitslice_rec) {
-        // Row-subset syndrome kernels (RSMI_BITSLICE_TOPS=0 keeps the full one, A/B runs).
+        // Row-subset syndrome kernels: opt-in (RSMI_BITSLICE_TOPS=1).  Same-box
+        // A/B, 20 steps x 3 reps (profiles/r03i/): the full kernel for every
+        // stripe is faster or tied on every config-5 mix (e = 1..4: 12.0 vs
+        // 12.4 ms; pool of 256: 15.2 vs 15.5 ms; 1..8 and 1..16: tied).
         const char* tv = std::getenv("RSMI_BITSLICE_TOPS");
-        c->n_tops = (tv && std::atoi(tv) == 0) ? 0 : c->bitslice->n_rec_tops;
+        c->n_tops = (tv && std::atoi(tv) != 0) ? c->bitslice->n_rec_tops : 0;
     }
     {
         // RS(64,16): with the network restricted to the rows a pattern uses,
