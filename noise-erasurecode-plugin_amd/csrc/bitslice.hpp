@@ -40,6 +40,17 @@ struct BitsliceArgs {
 
 using BitsliceLaunch = hipError_t (*)(const BitsliceArgs&, hipStream_t);
 
+// Per-descriptor record of what Rebuild does with the stripe's pattern
+// (k <= 64, m <= 32), written by the host next to the stripe descriptor so a
+// block knows which inputs to load from the same scalar load round trip as
+// its descriptor, with no dependent load of the pattern's id rows and no
+// ballots before its first data loads.
+struct alignas(16) BsStripeMask {
+    uint32_t dlo, dhi;  // bit j: data shard j present (it keeps its own slot)
+    uint32_t pmask;     // bit t: parity t is one of Rebuild's survivors (fills an erased data slot)
+    uint32_t qmask;     // bit t: parity t is erased (an output)
+};
+
 // Reconstruct launch: same stripe descriptors and pattern cache as the
 // split-table kernel (rs_kernels.hpp MatArgs).
 struct BitsliceRecArgs {
@@ -48,6 +59,7 @@ struct BitsliceRecArgs {
     uint64_t data_ss, parity_ss, pitch;
     uint64_t count;              // descriptors
     const uint2* stripe_desc;    // [count] {stripe, pattern id << 8 | outputs}
+    const BsStripeMask* stripe_mask;  // [count] the descriptors' mask records
     const uint8_t* coef;         // [npat][m][k] decode rows
     const uint32_t* src;         // [npat][k] survivor ids (Rebuild's slots)
     const uint32_t* dst;         // [npat][dst_stride] output ids

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     // load); encode (no table) is stripe sv, pattern 0, all m parity rows.
     uint2 desc = make_uint2(static_cast<uint32_t>(sv), a.m);
     if (a.stripe_desc) desc = a.stripe_desc[sv];
-    const uint64_t s = __builtin_amdgcn_readfirstlane(desc.x);
+    const uint64_t s = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(desc.x));
     const uint32_t sw = __builtin_amdgcn_readfirstlane(desc.y);
     const uint32_t pat = sw >> 8;
     const int e = static_cast<int>(sw & 0xFFu);
@@ -385,11 +385,14 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(const uint8_t* src, ui
     const uint32_t piece = blockIdx.x / chunks;
     const uint32_t col = (blockIdx.x - piece * chunks) * 256u + threadIdx.x;
     if (col >= cols16) return;
-    const uint64_t so = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pieces[2 * piece])) |
-                        (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pieces[2 * piece] >> 32))) << 32);
+    // readfirstlane returns int: the low words go through uint32_t, or an
+    // offset with bit 31 set would sign-extend over the high word.
+    const uint64_t s0 = pieces[2 * piece];
+    const uint64_t so = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s0))) |
+                        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s0 >> 32)))) << 32);
     const uint64_t d0 = pieces[2 * piece + 1];
-    const uint64_t dof = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(d0)) |
-                         (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(d0 >> 32))) << 32);
+    const uint64_t dof = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(d0))) |
+                         (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(d0 >> 32)))) << 32);
     const uint4 v = gload16<true>(src + so + static_cast<uint64_t>(col) * 16u);
     gstore16<true>(dst + dof + static_cast<uint64_t>(col) * 16u, v);
 }

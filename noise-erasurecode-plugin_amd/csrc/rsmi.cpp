@@ -278,6 +278,7 @@ struct rs_ctx {
     rsmi::PatIndex pat_index;
     std::vector<uint32_t> h_cnt;  // [npat] erased count of each pattern
     std::vector<uint8_t> h_lo;    // [npat] lowest parity row the pattern uses (m: none)
+    std::vector<rsmi::BsStripeMask> h_mask;  // [npat] Rebuild's slots and rows (bit-sliced reconstruct)
     int n_tops = 0;               // row-subset syndrome kernels in use (RSMI_BITSLICE_TOPS=0: none)
     std::vector<PatKey> h_key;    // keys of the patterns created since the last flush
     GrowBuf d_pcoef, d_psrc, d_pdst, d_pcnt, d_pstat, d_pkey;
@@ -488,10 +489,38 @@ int lowest_parity_row(const PatKey& key, int k, int n) {
     return lo;
 }
 
+// The syndrome kernel's mask record of a pattern (bitslice.hpp
+// BsStripeMask; k <= 64, m <= 32, zeros otherwise): present data shards,
+// Rebuild's parity survivors -- the d highest-numbered present parity rows,
+// d = erased data shards -- and the erased parity rows.
+rsmi::BsStripeMask stripe_mask(const PatKey& key, int k, int n) {
+    const int m = n - k;
+    rsmi::BsStripeMask r{0u, 0u, 0u, 0u};
+    if (k > 64 || m > 32) return r;
+    uint64_t present = 0;
+    int d = 0;
+    for (int i = 0; i < k; ++i) {
+        if (key.has(i)) ++d;
+        else present |= 1ull << i;
+    }
+    for (int t = m - 1; t >= 0; --t) {
+        if (key.has(k + t)) {
+            r.qmask |= 1u << t;
+        } else if (d > 0) {
+            r.pmask |= 1u << t;
+            --d;
+        }
+    }
+    r.dlo = static_cast<uint32_t>(present);
+    r.dhi = static_cast<uint32_t>(present >> 32);
+    return r;
+}
+
 int create_pattern(rs_ctx* c, const PatKey& key, int e) {
     const int id = static_cast<int>(c->h_cnt.size());
     c->h_cnt.push_back(static_cast<uint32_t>(e));
     c->h_lo.push_back(static_cast<uint8_t>(lowest_parity_row(key, c->k, c->n)));
+    c->h_mask.push_back(stripe_mask(key, c->k, c->n));
     c->h_key.push_back(key);
     c->pat_index.insert(key, id);
     return id;
@@ -565,6 +594,7 @@ void evict_patterns(rs_ctx* c) {
     c->h_key.clear();
     c->h_cnt.clear();
     c->h_lo.clear();
+    c->h_mask.clear();
     c->uploaded = 0;
     ++c->evictions;
 }
@@ -577,6 +607,7 @@ void rollback_patterns(rs_ctx* c) {
     c->pat_index.drop_from(static_cast<int>(c->uploaded));
     c->h_cnt.resize(c->uploaded);
     c->h_lo.resize(c->uploaded);
+    c->h_mask.resize(c->uploaded);
     c->h_key.clear();
 }
 
@@ -716,11 +747,19 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         ++count[kk];
         if (kk == 0) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
     }
-    if (!L.st_stripe.acquire(used * sizeof(uint2))) return RS_ENOMEM;
+    // Descriptors, then (for the syndrome kernels) each descriptor's mask
+    // record, in one upload.
+    const bool masks = used > count[0];
+    const size_t mask_off = round_up(used * sizeof(uint2), 16);
+    const size_t desc_bytes = masks ? mask_off + used * sizeof(rsmi::BsStripeMask) : used * sizeof(uint2);
+    if (!L.st_stripe.acquire(desc_bytes)) return RS_ENOMEM;
     uint2* desc = static_cast<uint2*>(L.st_stripe.p);
+    rsmi::BsStripeMask* mrec =
+        reinterpret_cast<rsmi::BsStripeMask*>(static_cast<uint8_t*>(L.st_stripe.p) + mask_off);
     auto put = [&](size_t slot, size_t i) {
         const uint32_t p = pid[i];
         desc[slot] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
+        if (masks) mrec[slot] = c->h_mask[p];
     };
     if (nb <= 4 * stripes + 4096) {
         std::vector<uint32_t>& start = L.start;
@@ -753,8 +792,8 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     }
     L.begin(s);  // the descriptor buffer's previous readers
     wait_patterns(c, s);
-    if (!L.d_stripe_pat.reserve_on(used * sizeof(uint2), s)) return RS_ENOMEM;
-    hipError_t e = hipMemcpyAsync(L.d_stripe_pat.p, desc, used * sizeof(uint2), hipMemcpyHostToDevice, s);
+    if (!L.d_stripe_pat.reserve_on(desc_bytes, s)) return RS_ENOMEM;
+    hipError_t e = hipMemcpyAsync(L.d_stripe_pat.p, desc, desc_bytes, hipMemcpyHostToDevice, s);
     L.st_stripe.release_after(s);
     if (e != hipSuccess) return RS_EDEVICE;
     const uint2* d_desc = static_cast<const uint2*>(L.d_stripe_pat.p);
@@ -780,6 +819,8 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.pitch = a.pitch;
         b.count = a.stripes;
         b.stripe_desc = d_desc + first;
+        b.stripe_mask = reinterpret_cast<const rsmi::BsStripeMask*>(static_cast<const uint8_t*>(L.d_stripe_pat.p) +
+                                                                    mask_off) + first;
         b.coef = a.coef;
         b.src = a.src;
         b.dst = a.dst;

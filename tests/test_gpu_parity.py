@@ -363,7 +363,7 @@ def test_row_subset_syndrome_kernels(S, pitch):
         assert torch.equal(pv[:, :, :S], pv0[:, :, :S]), f.kernel_name(1)
     # and in pointer mode, every shard at a random row of a pool
     _check_ptrs_roundtrip(f_top, k, n, S, er, 77 + S)
-    f_full.close()
+    f_top.close()  # the env-built context; f_full is the shared cached one
 
 
 def _check_ptrs_roundtrip(f, k, n, S, er, seed):

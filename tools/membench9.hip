@@ -82,6 +82,42 @@ __global__ __launch_bounds__(256) void rec(u32x4* __restrict__ data, u32x4* __re
         if (t < (int)e) st(shard(p.dst[t]) + col, acc[t]);
 }
 
+// The same with the pattern inlined in a 32-byte descriptor (survivor and
+// output ids as bytes): one scalar round trip before the survivor loads
+// instead of descriptor -> pattern (the engine's chain).  Measures what
+// shortening the prologue's dependent loads could buy.
+struct DescX {
+    uint32_t s, e;
+    uint8_t src[16];
+    uint8_t dst[8];
+};
+
+__global__ __launch_bounds__(256) void rec_inline(u32x4* __restrict__ data, u32x4* __restrict__ par, size_t pitch,
+                                                  const DescX* __restrict__ desc, uint32_t chunks, int xcd) {
+    const uint32_t L = logical(blockIdx.x, gridDim.x, chunks, xcd != 0);
+    const DescX& d = desc[L / chunks];
+    const uint32_t chunk = L % chunks;
+    const size_t s = __builtin_amdgcn_readfirstlane(d.s);
+    const uint32_t e = __builtin_amdgcn_readfirstlane(d.e);
+    auto shard = [&](uint32_t id) -> u32x4* {
+        return id < K ? data + (s * K + id) * pitch : par + (s * M + (id - K)) * pitch;
+    };
+    const size_t col = size_t(chunk) * 256 + threadIdx.x;
+    u32x4 acc[M];
+#pragma unroll
+    for (int t = 0; t < M; ++t) acc[t] = u32x4{0u, 0u, 0u, (unsigned)t};
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld(shard(__builtin_amdgcn_readfirstlane(d.src[j])) + col);
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int t = 0; t < M; ++t) acc[t] ^= x[j] << ((t + j) & 7);
+#pragma unroll
+    for (int t = 0; t < M; ++t)
+        if (t < (int)e) st(shard(__builtin_amdgcn_readfirstlane(d.dst[t])) + col, acc[t]);
+}
+
 // Rebuild's survivors: slot i takes shard i if present, else the highest remaining.
 static Pat make_pat(const std::vector<int>& erased) {
     Pat p{};
@@ -179,7 +215,44 @@ int main(int argc, char** argv) {
         CK(hipEventDestroy(a));
         CK(hipEventDestroy(b));
     };
+    DescX* d_descx;
+    CK(hipMalloc(&d_descx, stripes * sizeof(DescX)));
+    auto run_inline = [&](const std::vector<uint32_t>& pid, int xcd, double bytes, const char* name) {
+        std::vector<uint2> order(stripes);
+        for (int s = 0; s < stripes; ++s) order[s] = make_uint2(s, pid[s]);
+        std::stable_sort(order.begin(), order.end(), [](uint2 a, uint2 b) { return a.y < b.y; });
+        std::vector<DescX> dx(stripes);
+        for (int i = 0; i < stripes; ++i) {
+            const Pat& p = pats[order[i].y];
+            DescX& d = dx[i];
+            d = DescX{};
+            d.s = order[i].x;
+            d.e = p.e;
+            for (int j = 0; j < K; ++j) d.src[j] = static_cast<uint8_t>(p.src[j]);
+            for (int t = 0; t < M; ++t) d.dst[t] = static_cast<uint8_t>(p.dst[t]);
+        }
+        CK(hipMemcpy(d_descx, dx.data(), stripes * sizeof(DescX), hipMemcpyHostToDevice));
+        const dim3 g(stripes * chunks);
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        hipLaunchKernelGGL(rec_inline, g, dim3(256), 0, 0, data, par, pitch, d_descx, chunks, xcd);
+        CK(hipDeviceSynchronize());
+        const int reps = 5;
+        CK(hipEventRecord(a));
+        for (int r = 0; r < reps; ++r)
+            hipLaunchKernelGGL(rec_inline, g, dim3(256), 0, 0, data, par, pitch, d_descx, chunks, xcd);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        ms /= reps;
+        printf("%-34s %-8s %-10s %8.3f ms %8.1f GB/s\n", name, "inline", xcd ? "xcd" : "natural", ms, bytes / ms / 1e6);
+        CK(hipEventDestroy(a));
+        CK(hipEventDestroy(b));
+    };
     for (int rep = 0; rep < 2; ++rep) {
+        run_inline(mix, 1, mix_bytes, "random 1-4 erasures (headline)");
         run(mix, true, 1, mix_bytes, "random 1-4 erasures (headline)");
         run(mix, true, 0, mix_bytes, "random 1-4 erasures (headline)");
         run(mix, false, 1, mix_bytes, "random 1-4 erasures (headline)");
