@@ -24,7 +24,11 @@ the timed region at every N).
 
 `--gpus N` with N > 1 and no launcher starts N ranks itself
 (torch.distributed.run as a child process, the JSON line relayed); under a
-launcher, WORLD_SIZE must equal --gpus.
+launcher, WORLD_SIZE must equal --gpus.  At N > 1 the same ranks then run a
+short shard-distributed leg (configs[3]: the RCCL survivor gather and the
+pointer-mode reconstruct, checked on a sample) reported as "gather" -- never
+part of value, and abandoned by a per-rank watchdog rather than allowed to
+cost the headline line.
 """
 from __future__ import annotations
 
@@ -77,6 +81,13 @@ def parse():
     ap.add_argument("--stream-chunk", type=int, default=32, help="stripes per streamed chunk")
     ap.add_argument("--chunks", type=int, default=8,
                     help="sharded placement: exchange chunks per step (two chunks' buffers live)")
+    ap.add_argument("--gather-stripes", type=int, default=512,
+                    help="N > 1, local placement: after the timed region (and the CPU baseline), "
+                         "a short shard-distributed leg with this many owned stripes per rank "
+                         "runs the RCCL survivor gather + pointer reconstruct and checks it "
+                         "(configs[3]); reported as 'gather', never 'value'. 0 disables")
+    ap.add_argument("--gather-timeout", type=float, default=180.0,
+                    help="seconds after which a stuck gather leg is abandoned (the line is still printed)")
     return ap.parse_args()
 
 
@@ -410,6 +421,7 @@ def main():
         pass
 
     local_bytes = step_bytes_local
+    out = None
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:  # after the timed region, on rank 0, at every N
@@ -468,9 +480,78 @@ def main():
                           "encode_ms": round(v[1], 3), "reconstruct_ms": round(v[2], 3)}
                          for r, v in enumerate(per_rank)],
         }
+    if distributed and world > 1 and args.gather_stripes > 0:
+        # configs[3]'s survivor gather on the same ranks, after the headline
+        # is measured: its own buffers, so the local ones go first.
+        del data, parity
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        gather_leg(args, f, k, n, S, emax, world, rank, dev, out)  # emits the line and tears down
+        return
+    if rank == 0:
         emit(out)
     if distributed:
         torch.distributed.destroy_process_group()
+
+
+def gather_leg(args, f, k, n, S, emax, world, rank, dev, out):
+    """N > 1: a short shard-distributed leg (sharded_run with
+    --gather-stripes owned stripes per rank, 1 warm-up + 2 timed steps,
+    every step checked on a sample) reported as out["gather"].  A watchdog
+    per rank abandons a leg stuck in a collective after --gather-timeout
+    seconds: rank 0 still prints the headline line (gather.status says
+    what happened) and every rank exits, so the headline measurement is
+    never lost to the extra leg.  Wrong shards exit non-zero after the
+    line is printed."""
+    import threading
+
+    lock = threading.Lock()
+    state = {"emitted": False}
+
+    def finish(gather):
+        with lock:
+            if state["emitted"]:
+                return False
+            state["emitted"] = True
+        if rank == 0 and out is not None:
+            out["gather"] = gather
+            emit(out)
+        return True
+
+    def abandon():
+        if finish({"status": f"abandoned after {args.gather_timeout:.0f} s (collective did not complete)"}):
+            sys.stderr.write("bench.py: gather leg abandoned\n")
+            sys.stderr.flush()
+            os._exit(0)
+
+    torch.distributed.barrier()  # rank 0's CPU baseline is done: start every clock together
+    timer = threading.Timer(args.gather_timeout, abandon)
+    timer.daemon = True
+    timer.start()
+    steps, warmup = 2, 1
+    gather = {"status": "ok", "owned_stripes_per_rank": args.gather_stripes, "shard_bytes": S,
+              "steps": steps, "warmup": warmup,
+              "what": "shard i of every stripe on rank i mod N; each owner gathers exactly Rebuild's "
+                      "survivors over RCCL (batch_isend_irecv) and reconstructs from the receive buffers "
+                      "(rs_reconstruct_ptrs); not part of value"}
+    bad = 0
+    try:
+        res = sharded_run(f, k, n, S, args.gather_stripes, steps, warmup, args.emin, emax, 0, args.chunks,
+                          world, rank, dev, True, budget_exit=False)
+        if res is None:
+            gather["status"] = "skipped: HBM budget"
+        else:
+            gather.update(gather_summary(res, steps, world))
+            bad = res["verified"]["mismatched_shards"]
+            if bad:
+                gather["status"] = "wrong shards"
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # reported; the headline line is still printed
+        gather["status"] = f"error: {type(e).__name__}: {e}"
+    timer.cancel()
+    finish(gather)
+    if bad:
+        raise SystemExit("bench.py: the gather leg reconstructed wrong shards")
 
 
 def stream_main(args, world, rank, local, dev, distributed):
@@ -549,35 +630,32 @@ def stream_main(args, world, rank, local, dev, distributed):
         torch.distributed.destroy_process_group()
 
 
-def sharded_main(args, world, rank, local, dev, distributed):
+def sharded_run(f, k, n, S, stripes, steps, warmup, emin, emax, pool, chunks, world, rank, dev, distributed,
+                budget_exit=True):
     """configs[3], shard-distributed placement: shard i of every stripe is
     held by rank i mod N (the p2p analogue of main.go:207 broadcasting each
     shard to peers).  One step = the survivor gather (exactly the survivors
-    each owner reads, rsmi/distributed.py) in --chunks chunks, chunk c + 1's
+    each owner reads, rsmi/distributed.py) in `chunks` chunks, chunk c + 1's
     RCCL exchange (communication stream) overlapping chunk c's
     rs_reconstruct_ptrs (compute stream), which reads survivors where they
     landed.  The per-rank HBM budget is computed before anything is
-    allocated; a budget over the free HBM raises --chunks, and exits
-    non-zero with the numbers if even that cannot fit.  Reported against
-    the xGMI roofline (gathered bytes)."""
-    import rsmi
+    allocated; a budget over the free HBM raises the chunk count, and past
+    64 chunks exits non-zero with the numbers (budget_exit) or returns None.
+    Every rank returns the all-gathered per-rank statistics and the summary."""
     from rsmi import distributed as rd
 
-    k, n, S = args.k, args.n, args.shard
     m = n - k
-    emax = args.emax if args.emax is not None else m
-    gstripes = args.stripes * world          # global stripes; each rank owns args.stripes
-    f = rsmi.FEC(k, n, device=local)
+    gstripes = stripes * world           # global stripes; each rank owns `stripes`
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     ids = rd.local_shard_ids(rank, n, world)
     rng = np.random.default_rng(0xE4A5)  # same erasure map on every rank
-    ersets = erasure_sets(rng, args.warmup + args.steps, gstripes, n, args.emin, emax, args.pattern_pool)
+    ersets = erasure_sets(rng, warmup + steps, gstripes, n, emin, emax, pool)
     # Plans first (host metadata, identical on every rank), then the budget.
     free_b, _ = torch.cuda.mem_get_info(dev)
     if os.environ.get("RSMI_BENCH_BACKEND", "nccl") != "nccl":
         free_b //= -(-world // max(torch.cuda.device_count(), 1))  # ranks share the rehearsal GPU(s)
-    chunks = max(1, args.chunks)
+    chunks = max(1, chunks)
     while True:
         tp = time.perf_counter()
         plans = [rd.plan_exchange(er, k, n, rank, world, S, chunks=chunks) for er in ersets]
@@ -590,7 +668,9 @@ def sharded_main(args, world, rank, local, dev, distributed):
         sys.stderr.write(f"bench.py: sharded placement needs {budget['total']:.1f} GB per rank "
                          f"({', '.join(f'{key} {v:.1f}' for key, v in budget.items() if key != 'total')}) "
                          f"but {free_b / 1e9:.1f} GB are free: lower --stripes\n")
-        raise SystemExit(3)
+        if budget_exit:
+            raise SystemExit(3)
+        return None
     held = torch.empty((gstripes, len(ids), S), dtype=torch.uint8, device=dev)
     # Setup (untimed): the global data is one splitmix stream, generated in
     # batches; a rank keeps the rows of its shard ids and encodes only when
@@ -621,22 +701,22 @@ def sharded_main(args, world, rank, local, dev, distributed):
     def step(i):
         rd.run_step(f, held, plans[i], bufs, tables[i], er_owned[i], S, stream, comm)
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         step(i)
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
+    for i in range(warmup, warmup + steps):
         step(i)
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     rec_bytes = sum(int(((k + ersets[i][plans[i].owned].sum(axis=1)) * S).sum())
-                    for i in range(args.warmup, args.warmup + args.steps))
-    xgmi_bytes = sum(plans[i].bytes_in for i in range(args.warmup, args.warmup + args.steps))
+                    for i in range(warmup, warmup + steps))
+    xgmi_bytes = sum(plans[i].bytes_in for i in range(warmup, warmup + steps))
     # Check (untimed) the last step's outputs on a sample of owned stripes:
     # each stripe regenerated from the global stream and encoded here, its
     # erased shards compared with what the gather + reconstruct produced.
@@ -661,39 +741,74 @@ def sharded_main(args, world, rank, local, dev, distributed):
         per_rank = [g.tolist() for g in gathered]
     else:
         per_rank = [mine.tolist()]
+    del held, bufs, tables
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
     elapsed = max(r[0] for r in per_rank)
-    rec_total = sum(r[1] for r in per_rank)
-    xgmi_total = sum(r[2] for r in per_rank)
+    return {"per_rank": per_rank, "elapsed": elapsed, "rec_total": sum(r[1] for r in per_rank),
+            "xgmi_total": sum(r[2] for r in per_rank), "chunks": len(plans[0].chunks), "budget": budget,
+            "free_b": free_b, "plan_ms": plan_ms, "rccl": rccl,
+            "verified": {"stripes": int(sum(r[5] for r in per_rank)),
+                         "mismatched_shards": int(sum(r[6] for r in per_rank)),
+                         "how": "last step, up to 16 owned stripes per rank regenerated and encoded locally"}}
+
+
+def gather_summary(res, steps, world):
+    """The survivor-gather leg's numbers (xGMI roofline: gathered bytes)."""
+    xg = res["xgmi_total"] / res["elapsed"] / 1e9
+    return {
+        "reconstruct_GBps": round(res["rec_total"] / res["elapsed"] / 1e9, 2),
+        "ms_per_step": round(res["elapsed"] / steps * 1e3, 3),
+        "xgmi": {"gathered_GB": round(res["xgmi_total"] / 1e9, 3),
+                 "gathered_GB_per_step": round(res["xgmi_total"] / steps / 1e9, 3),
+                 "achieved_GBps_total": round(xg, 1), "per_rank_GBps": round(xg / max(world, 1), 1),
+                 "link_peak_GBps": 153.0, "links_per_gpu": 7},
+        "chunks": res["chunks"],
+        "overlap": "RCCL exchange of chunk c+1 on a communication stream || reconstruct of chunk c"
+                   if res["rccl"] else "none (gloo rehearsal: chunks in sequence)",
+        "hbm_budget_GB": {key: round(v, 2) for key, v in res["budget"].items()},
+        "hbm_free_GB": round(res["free_b"] / 1e9, 1),
+        "plan_ms_per_step": round(res["plan_ms"], 2),
+        "verified": res["verified"],
+        "per_rank": [{"rank": r, "ms_per_step": round(v[0] / steps * 1e3, 3),
+                      "gathered_GB_per_step": round(v[2] / steps / 1e9, 3),
+                      "reconstruct_GBps": round(v[1] / v[0] / 1e9, 2),
+                      "hbm_budget_GB": round(v[3], 2), "plan_ms": round(v[4], 2)}
+                     for r, v in enumerate(res["per_rank"])],
+    }
+
+
+def sharded_main(args, world, rank, local, dev, distributed):
+    """configs[3] as its own run (--placement sharded): see sharded_run."""
+    import rsmi
+
+    k, n, S = args.k, args.n, args.shard
+    emax = args.emax if args.emax is not None else n - k
+    f = rsmi.FEC(k, n, device=local)
+    res = sharded_run(f, k, n, S, args.stripes, args.steps, args.warmup, args.emin, emax, args.pattern_pool,
+                      args.chunks, world, rank, dev, distributed)
     if rank == 0:
-        xg = xgmi_total / elapsed / 1e9
+        g = gather_summary(res, args.steps, world)
         emit({
             "metric": "RS(10,4) reconstruct GB/s with RCCL survivor gather (configs[3], sharded)",
-            "value": round(rec_total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "value": g["reconstruct_GBps"], "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "ms_per_step": g["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": f"RS({k},{n}) {args.emin}-{emax}-erasure reconstruct, shard i "
                                    f"on rank i mod N, {args.stripes} owned stripes x {S} B shards "
-                                   "per rank", "placement": "sharded", "chunks": len(plans[0].chunks),
-                       "overlap": "RCCL exchange of chunk c+1 on a communication stream || reconstruct of chunk c"
-                                  if rccl else "none (gloo rehearsal: chunks in sequence)"},
-            "xgmi": {"gathered_GB": round(xgmi_total / 1e9, 3), "gathered_GB_per_step": round(xgmi_total / args.steps / 1e9, 3),
-                     "achieved_GBps_total": round(xg, 1), "per_rank_GBps": round(xg / max(world, 1), 1),
-                     "link_peak_GBps": 153.0, "links_per_gpu": 7},
-            "hbm_budget_GB": {key: round(v, 2) for key, v in budget.items()},
-            "hbm_free_GB": round(free_b / 1e9, 1),
-            "plan_ms_per_step": round(plan_ms, 2),
-            "verified": {"stripes": int(sum(r[5] for r in per_rank)), "mismatched_shards": int(sum(r[6] for r in per_rank)),
-                         "how": "last step, up to 16 owned stripes per rank regenerated and encoded locally"},
-            "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),
-                          "gathered_GB_per_step": round(v[2] / args.steps / 1e9, 3),
-                          "reconstruct_GBps": round(v[1] / v[0] / 1e9, 2),
-                          "hbm_budget_GB": round(v[3], 2), "plan_ms": round(v[4], 2)}
-                         for r, v in enumerate(per_rank)],
+                                   "per rank", "placement": "sharded", "chunks": g["chunks"],
+                       "overlap": g["overlap"]},
+            "xgmi": g["xgmi"],
+            "hbm_budget_GB": g["hbm_budget_GB"],
+            "hbm_free_GB": g["hbm_free_GB"],
+            "plan_ms_per_step": g["plan_ms_per_step"],
+            "verified": g["verified"],
+            "per_rank": g["per_rank"],
         })
     if distributed:
         torch.distributed.destroy_process_group()
-    if sum(r[6] for r in per_rank):
+    if res["verified"]["mismatched_shards"]:
         raise SystemExit("bench.py: sharded reconstruct produced wrong shards")
 
 
