@@ -263,9 +263,14 @@ def test_bitslice_reconstruct_kernel_selection():
 
 def _fixed_patterns(k, n):
     """Edge erasure sets: every single erasure, all-data, all-parity, the
-    m highest data shards, alternating, and the first/last shard pairs."""
+    m highest data shards, alternating, the first/last shard pairs, and sets
+    straddling data shard 31/32 (the two words of the syndrome kernel's
+    present-data mask: a set bit 31 of the low word once sign-extended over
+    the high word, profiles/r03k/)."""
     m = n - k
     pats = [[i] for i in range(n)]
+    if k > 33:
+        pats += [[31, 32], [33, 40, k - 1], [30, 31, 32, 33][:m], [32, k][:m]]
     pats += [list(range(min(m, k))), list(range(k, n)), list(range(k - min(m, k), k)),
              list(range(0, n, 2))[:m], [0, n - 1], [k - 1, k]]
     out = np.zeros((len(pats), n), dtype=np.uint8)
