@@ -112,3 +112,28 @@ def test_self_launch_relays_one_json_line(monkeypatch, capsys):
     assert bench.self_launch(2, []) == 3
     monkeypatch.setattr(bench, "launch_command", lambda g, a, p: [sys.executable, "-c", "print('x')"])
     assert bench.self_launch(2, []) == 1  # exit 0 but no JSON line
+
+
+def test_gather_summary_arithmetic():
+    """The N > 1 gather leg's report (bench.gather_summary): totals over ranks
+    against the max-over-ranks time, per-rank rows, xGMI figures."""
+    per_rank = [[2.0, 40e9, 10e9, 12.5, 1.0, 16, 0], [1.6, 36e9, 8e9, 12.0, 1.2, 16, 0]]
+    res = {"per_rank": per_rank, "elapsed": 2.0, "rec_total": 76e9, "xgmi_total": 18e9, "chunks": 8,
+           "budget": {"held": 8.0, "total": 12.5}, "free_b": 280e9, "plan_ms": 0.5, "rccl": True,
+           "verified": {"stripes": 32, "mismatched_shards": 0, "how": "x"}}
+    g = bench.gather_summary(res, steps=2, world=2)
+    assert g["reconstruct_GBps"] == 38.0 and g["ms_per_step"] == 1000.0
+    assert g["xgmi"]["gathered_GB"] == 18.0 and g["xgmi"]["gathered_GB_per_step"] == 9.0
+    assert g["xgmi"]["achieved_GBps_total"] == 9.0 and g["xgmi"]["per_rank_GBps"] == 4.5
+    assert g["overlap"].startswith("RCCL")
+    assert [r["rank"] for r in g["per_rank"]] == [0, 1]
+    assert g["per_rank"][1]["ms_per_step"] == 800.0 and g["per_rank"][1]["reconstruct_GBps"] == 22.5
+    assert g["hbm_free_GB"] == 280.0 and g["verified"]["stripes"] == 32
+    res["rccl"] = False
+    assert bench.gather_summary(res, 2, 2)["overlap"].startswith("none")
+
+
+def test_gather_flags_pass_through_the_launcher():
+    argv = ["--gpus", "8", "--gather-stripes", "256", "--gather-timeout", "60"]
+    cmd = bench.launch_command(8, argv, 29500)
+    assert cmd[-len(argv):] == argv and "--nproc-per-node=8" in cmd
