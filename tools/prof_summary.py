@@ -149,8 +149,9 @@ def main():
             split = any("rs_matmul_kernel" in r["Kernel_Name"] for r in all_tr)
             variants = sorted({short_name(r["Kernel_Name"]) for r in rec})
             what = ("the split-table launch (stripes with e below RSMI_BITSLICE_REC_MIN_E) plus the syndrome launches"
-                    if split else f"the syndrome launches ({', '.join(f'`{v}`' for v in variants)}: each stripe in "
-                                  "the smallest row-subset kernel covering its pattern)")
+                    if split else (f"the syndrome launches ({', '.join(f'`{v}`' for v in variants)}: each stripe in "
+                                   "the smallest row-subset kernel covering its pattern)" if len(variants) > 1 else
+                                   f"the syndrome kernel `{variants[0]}`, every stripe"))
             # steps = encode launches (mode both) or, in reconstruct mode, launches of the full kernel
             steps = len(enc) if a.mode == "both" and enc else max(1, len([r for r in rec if "_t" not in short_name(r["Kernel_Name"])]))
             rms = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rec) / steps
