@@ -45,6 +45,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+# Exit status of a rank whose N > 1 gather leg was abandoned by its watchdog
+# (a collective that never completed): the headline line is printed first,
+# but the run must not read as a success.
+EXIT_GATHER_ABANDONED = 75
 
 
 def parse():
@@ -87,7 +91,15 @@ def parse():
                          "runs the RCCL survivor gather + pointer reconstruct and checks it "
                          "(configs[3]); reported as 'gather', never 'value'. 0 disables")
     ap.add_argument("--gather-timeout", type=float, default=180.0,
-                    help="seconds after which a stuck gather leg is abandoned (the line is still printed)")
+                    help="seconds after which a stuck gather leg is abandoned (the line is still printed, "
+                         f"then the ranks exit {EXIT_GATHER_ABANDONED})")
+    ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
+                    help="N = 1: skip the configs[0] (per-message latency) and configs[4] (RS(64,16)) "
+                         "legs reported beside the headline")
+    ap.add_argument("--config1-reps", type=int, default=50)
+    ap.add_argument("--config5-stripes", type=int, default=16384)
+    ap.add_argument("--config5-steps", type=int, default=5)
+    ap.add_argument("--config5-warmup", type=int, default=2)
     return ap.parse_args()
 
 
@@ -110,6 +122,13 @@ def erasure_sets(rng, count, stripes, n, emin, emax, pool=0):
 def pattern_total(n, emax):
     from math import comb
     return sum(comb(n, e) for e in range(1, emax + 1))
+
+
+def job_totals(per_rank):
+    """(job seconds, job bytes) from the all-gathered per-rank rows
+    [seconds, ..., bytes]: the slowest rank's time and every rank's own
+    algorithmic bytes summed (value = bytes / seconds)."""
+    return max(r[0] for r in per_rank), sum(r[-1] for r in per_rank)
 
 
 def host_cpu_info():
@@ -281,6 +300,230 @@ def self_launch(gpus: int, argv) -> int:
     return rc
 
 
+def device_run(f, k, n, S, stripes, steps, warmup, ersets, do_enc, do_rec, dev, seed=0x5EED,
+               prepare_emax=None, distributed=False):
+    """The device-resident hot path: `stripes` stripes of RS(k, n) with
+    S-byte shards allocated and filled in HBM (splitmix64, untimed), then
+    `warmup` untimed and `steps` timed steps, each = rs_encode_stripes of
+    every stripe and/or rs_reconstruct_stripes with that step's erasure
+    flags (ersets[i], host -> pattern lookup and upload inside the step).
+    Timed region bracketed by synchronize (+ barrier when distributed); HIP
+    events on the launch stream time each kernel.  The buffers are freed
+    before returning.  When every pattern of <= prepare_emax erasures fits
+    the ctx cache they are built before timing (prep_ms)."""
+    m = n - k
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    data = torch.empty(stripes * k * S, dtype=torch.uint8, device=dev)
+    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device=dev)
+    f.fill_splitmix(data.data_ptr(), data.numel(), seed, sh)
+    f.fill_splitmix(parity.data_ptr(), parity.numel(), 1, sh)
+    prep_ms = None
+    if prepare_emax is not None and pattern_total(n, prepare_emax) <= (1 << 20):
+        # Every pattern inverted on the GPU + uploaded once, before timing (a
+        # context keeps them cached for its lifetime); its one-off cost is
+        # reported as breakdown.pattern_prepare_ms.
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter()
+        f.prepare_patterns(prepare_emax, sh)
+        torch.cuda.synchronize(dev)
+        prep_ms = (time.perf_counter() - tp) * 1e3
+    if not do_enc:  # reconstruct needs valid parity once
+        f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, sh)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+
+    def step(i, timed):
+        e = ev[i - warmup] if timed else None
+        if e:
+            e[0].record(stream)
+        if do_enc:
+            f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, sh)
+        if e:
+            e[1].record(stream)
+        if do_rec:
+            f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                                  ersets[i].tobytes(), sh)
+        if e:
+            e[2].record(stream)
+
+    for i in range(warmup):
+        step(i, False)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + steps):
+        step(i, True)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    res = {"elapsed": elapsed, "encode_ms": [a.elapsed_time(b) for a, b, _ in ev],
+           "reconstruct_ms": [b.elapsed_time(c) for _, b, c in ev], "prep_ms": prep_ms}
+    del data, parity
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return res
+
+
+def guarded_leg(fn):
+    """Runs an extra (non-headline) leg; a failure is reported in the line
+    instead of costing the headline measurement."""
+    try:
+        return fn()
+    except Exception as e:  # reported, never silent
+        return {"status": f"error: {type(e).__name__}: {e}"}
+
+
+def _median_ms(fn, reps):
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return round(float(np.median(ts)) * 1e3, 4)
+
+
+def config1_leg(local, reps=50):
+    """configs[0]: the reference's own per-message call pattern.  The
+    1,048,580-B blob (1 MiB of splitmix64 bytes zero-padded to a multiple
+    of k = 10) is encoded once per call the way
+    shardInput does (main.go:243-267) and decoded from 10 of its 14 shares
+    after 4 seeded drops the way Receive does (main.go:72-79).  Timed as the
+    median of `reps` calls:
+      * codec: rs_encode / rs_decode at the C ABI on caller-owned pageable
+        buffers (what the cgo shim hands over; PCIe-inclusive);
+      * plugin: the C++ ShardPlugin mirror -- prepareShards into 14 Shard
+        messages (no signer), and 10 Receive calls whose last one decodes
+        (no verifier), through its Python binding;
+      * cpu: the oracle on 1 thread for the same blob (scalar mul_table and
+        AVX2 split-nibble addmul: encode, and Rebuild of the dropped data
+        shards).
+    Outputs are checked against the oracle / the blob."""
+    import ctypes
+
+    import rsmi
+    from oracle import oracle
+    from rsmi import host as h
+
+    k, n = 10, 14
+    m = n - k
+    blob_np = np.concatenate([oracle.splitmix_bytes(1 << 20, 0x5EED), np.zeros(4, dtype=np.uint8)])
+    L = blob_np.size
+    S = L // k
+    lib = rsmi.load()
+    f = rsmi.FEC(k, n, device=local)
+    P = ctypes.c_void_p
+    parity = np.zeros(m * S, dtype=np.uint8)
+    enc_ms = _median_ms(lambda: lib.rs_encode(f.handle, P(blob_np.ctypes.data), L, P(parity.ctypes.data)), reps)
+    E = oracle.fec_matrix(k, n)
+    ref_par = np.frombuffer(oracle.encode(E, k, n, blob_np.tobytes()), dtype=np.uint8)
+    if not np.array_equal(parity, ref_par):
+        raise RuntimeError("config1: rs_encode parity differs from the oracle")
+    rng = np.random.default_rng(0xC0F1)
+    lost = sorted(int(v) for v in rng.choice(n, size=4, replace=False))
+    keep = [i for i in range(n) if i not in lost]
+    shard = lambda i: blob_np[i * S:(i + 1) * S] if i < k else parity[(i - k) * S:(i - k + 1) * S]
+    bufs = [np.ascontiguousarray(shard(i)) for i in keep]
+    dst = np.zeros(L, dtype=np.uint8)
+
+    def dec():
+        nums = (ctypes.c_int * k)(*keep)
+        ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
+        rc = lib.rs_decode(f.handle, nums, ptrs, k, S, P(dst.ctypes.data))
+        if rc:
+            raise RuntimeError(f"config1: rs_decode returned {rc}")
+    dec_ms = _median_ms(dec, reps)
+    if not np.array_equal(dst, blob_np):
+        raise RuntimeError("config1: rs_decode did not return the blob")
+    # plugin mirror: prepareShards -> 14 Shards; 10 Receives, the last decodes
+    blob = blob_np.tobytes()
+    me = h.PeerID("tcp://localhost:3000", b"\x11" * 32)
+    sender = h.NewShardPlugin(None, None, k, n)
+    wires = [s_.Marshal() for s_ in sender.prepareShards(me, blob)]
+    if len(wires) != n:
+        raise RuntimeError("config1: prepareShards did not return 14 shards")
+    prep_ms = _median_ms(lambda: sender.prepareShards(me, blob), reps)
+    msgs = []
+    for i in keep:
+        s_ = h.Shard()
+        s_.Unmarshal(wires[i])
+        msgs.append(s_)
+
+    def receive():
+        r = h.NewShardPlugin(None, None, k, n)
+        ev = None
+        for s_ in msgs:
+            ev = r.Receive(me, s_)
+        if not ev.decoded or ev.message != blob:
+            raise RuntimeError("config1: Receive did not decode the blob")
+    recv_ms = _median_ms(receive, reps)
+    # the oracle on one thread, same blob
+    cpu = {}
+    er = np.zeros((1, n), dtype=np.uint8)
+    er[0, [i for i in lost if i < k]] = 1  # Rebuild regenerates the dropped data shares only
+    par = np.zeros(m * S, dtype=np.uint8)
+    for name, simd in (("scalar_1t", False), ("avx2_1t", True)):
+        e_ms = _median_ms(lambda: oracle.encode_batch(E, k, n, blob_np, S, 1, simd=simd, threads=1, out=par),
+                          max(5, reps // 5))
+        work = blob_np.copy()
+        d_ms = _median_ms(lambda: oracle.reconstruct_batch(E, k, n, work, par, S, 1, er, simd=simd, threads=1),
+                          max(5, reps // 5))
+        cpu[name] = {"encode_ms": e_ms, "decode4_ms": d_ms}
+    best = min(cpu.values(), key=lambda v: v["encode_ms"])
+    return {
+        "status": "ok",
+        "what": "configs[0]: 1,048,580-B blob, RS(10,4), one call per message (main.go:243-267 encode, "
+                "main.go:72-79 decode after 4 seeded drops); median latency; PCIe-inclusive",
+        "message_bytes": L, "shard_bytes": S, "dropped": lost, "reps": reps,
+        "codec": {"encode_ms": enc_ms, "decode4_ms": dec_ms,
+                  "encode_GBps": round(L * n / k / enc_ms / 1e6, 2)},
+        "plugin": {"prepareShards_ms": prep_ms, "receive10_decode_ms": recv_ms,
+                   "note": "C++ ShardPlugin mirror through pybind (blob and 14 shards copied across the "
+                           "binding); no signer / verifier"},
+        "cpu_1t": cpu,
+        "gpu_vs_1core": {"encode": round(best["encode_ms"] / enc_ms, 3),
+                         "decode4": round(min(v["decode4_ms"] for v in cpu.values()) / dec_ms, 3)},
+    }
+
+
+def config5_leg(local, dev, stripes=16384, steps=5, warmup=2):
+    """configs[4]: the wide code RS(64,16) with 64 KiB shards, `stripes`
+    stripes (64 x 64 KiB = 4 MiB of data each) device-resident, a fresh
+    1-16-erasure set per step (patterns inverted on the GPU inside the step,
+    the pattern space is too large to prepare).  Encode and reconstruct
+    times from HIP events, GB/s on the algorithmic bytes and the fraction of
+    the HBM roofline."""
+    import rsmi
+    k, n, S = 64, 80, 65536
+    m = n - k
+    f = rsmi.FEC(k, n, device=local)
+    rng = np.random.default_rng(0xE4A5)
+    ersets = erasure_sets(rng, warmup + steps, stripes, n, 1, m)
+    run = device_run(f, k, n, S, stripes, steps, warmup, ersets, True, True, dev)
+    enc_bytes = stripes * n * S
+    rec_bytes = sum(int(((k + er.sum(axis=1)) * S).sum()) for er in ersets[warmup:]) / steps
+    enc_ms = sum(run["encode_ms"]) / steps
+    rec_ms = sum(run["reconstruct_ms"]) / steps
+    enc_gbps = enc_bytes / (enc_ms / 1e3) / 1e9
+    rec_gbps = rec_bytes / (rec_ms / 1e3) / 1e9
+    return {
+        "status": "ok",
+        "what": f"configs[4]: RS(64,16), {stripes} stripes x 64 x 64 KiB shards, fresh 1-16 erasures per "
+                "stripe per step (patterns built on the GPU inside the step)",
+        "steps": steps, "warmup": warmup, "stripes": stripes, "shard_bytes": S,
+        "ms_per_step": round(run["elapsed"] / steps * 1e3, 3),
+        "value_GBps": round((enc_bytes + rec_bytes) / (run["elapsed"] / steps) / 1e9, 1),
+        "encode": {"kernel": f.kernel_name(0), "ms": round(enc_ms, 3), "GBps": round(enc_gbps, 1),
+                   "frac": round(enc_gbps / HBM_PEAK_GBS, 4), "bytes": enc_bytes},
+        "reconstruct": {"kernel": f.kernel_name(1), "ms": round(rec_ms, 3), "GBps": round(rec_gbps, 1),
+                        "frac": round(rec_gbps / HBM_PEAK_GBS, 4), "bytes": int(rec_bytes)},
+    }
+
+
 def main():
     global _RESULT_OUT
     args = parse()
@@ -323,24 +566,7 @@ def main():
     emax = args.emax if args.emax is not None else m
     stripes = args.stripes
     f = rsmi.FEC(k, n, device=local)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
-
-    data = torch.empty(stripes * k * S, dtype=torch.uint8, device=dev)
-    parity = torch.empty(stripes * m * S, dtype=torch.uint8, device=dev)
-    f.fill_splitmix(data.data_ptr(), data.numel(), 0x5EED ^ (rank << 32), sh)
-    f.fill_splitmix(parity.data_ptr(), parity.numel(), 1, sh)
     pool = args.pattern_pool
-    prep_ms = None
-    if pattern_total(n, emax) <= (1 << 20):
-        # Every pattern inverted on the GPU + uploaded once, before timing (a
-        # context keeps them cached for its lifetime); its one-off cost is
-        # reported as breakdown.pattern_prepare_ms.
-        torch.cuda.synchronize(dev)
-        tp = time.perf_counter()
-        f.prepare_patterns(emax, sh)
-        torch.cuda.synchronize(dev)
-        prep_ms = (time.perf_counter() - tp) * 1e3
     rng = np.random.default_rng(0xE4A5 + rank)
     if args.erase:
         fixed = np.zeros((stripes, n), dtype=np.uint8)
@@ -350,47 +576,17 @@ def main():
         ersets = erasure_sets(rng, args.warmup + args.steps, stripes, n, args.emin, emax, pool)
     rec_bytes = [int(((k + er.sum(axis=1)) * S).sum()) for er in ersets]
     enc_bytes = stripes * (k + m) * S
-
     do_enc = args.mode in ("both", "encode")
     do_rec = args.mode in ("both", "reconstruct")
-    if not do_enc:  # reconstruct needs valid parity once
-        f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, sh)
-
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-
-    def step(i, timed):
-        e = ev[i - args.warmup] if timed else None
-        if e:
-            e[0].record(stream)
-        if do_enc:
-            f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, sh)
-        if e:
-            e[1].record(stream)
-        if do_rec:
-            f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
-                                  ersets[i].tobytes(), sh)
-        if e:
-            e[2].record(stream)
-
-    for i in range(args.warmup):
-        step(i, False)
-    torch.cuda.synchronize(dev)
-    if distributed:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
-        step(i, True)
-    torch.cuda.synchronize(dev)
-    if distributed:
-        torch.distributed.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    enc_ms = [a.elapsed_time(b) for a, b, _ in ev]
-    rec_ms = [b.elapsed_time(c) for _, b, c in ev]
-    # Per-rank wall time and kernel times; the job's time is the max.
-    mine = torch.tensor([elapsed, sum(enc_ms) / len(enc_ms), sum(rec_ms) / len(rec_ms)],
+    run = device_run(f, k, n, S, stripes, args.steps, args.warmup, ersets, do_enc, do_rec, dev,
+                     seed=0x5EED ^ (rank << 32), prepare_emax=emax, distributed=distributed)
+    elapsed, enc_ms, rec_ms, prep_ms = run["elapsed"], run["encode_ms"], run["reconstruct_ms"], run["prep_ms"]
+    # Per-rank wall time, kernel times and algorithmic bytes (each rank draws
+    # its own erasure sets, so its reconstruct bytes are its own); the job's
+    # time is the max over ranks, its bytes the sum.
+    step_bytes_local = sum((enc_bytes if do_enc else 0) + (rec_bytes[i] if do_rec else 0)
+                           for i in range(args.warmup, args.warmup + args.steps))
+    mine = torch.tensor([elapsed, sum(enc_ms) / len(enc_ms), sum(rec_ms) / len(rec_ms), step_bytes_local],
                         dtype=torch.float64, device=stats_device(dev))
     if distributed:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
@@ -398,10 +594,7 @@ def main():
         per_rank = [g.tolist() for g in gathered]
     else:
         per_rank = [mine.tolist()]
-    elapsed = max(r[0] for r in per_rank)
-    step_bytes_local = sum((enc_bytes if do_enc else 0) + (rec_bytes[i] if do_rec else 0)
-                           for i in range(args.warmup, args.warmup + args.steps))
-    total_bytes = step_bytes_local * world
+    elapsed, total_bytes = job_totals(per_rank)
     value = total_bytes / elapsed / 1e9
 
     enc_avg_ms = sum(enc_ms) / len(enc_ms)
@@ -420,7 +613,6 @@ def main():
     except (OSError, ValueError):
         pass
 
-    local_bytes = step_bytes_local
     out = None
     if rank == 0:
         cpu = None
@@ -476,64 +668,98 @@ def main():
             },
             "cpu_baseline": cpu,
             "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),
-                          "value": round(local_bytes / v[0] / 1e9, 2),
+                          "value": round(v[3] / v[0] / 1e9, 2), "bytes": int(v[3]),
                           "encode_ms": round(v[1], 3), "reconstruct_ms": round(v[2], 3)}
                          for r, v in enumerate(per_rank)],
         }
     if distributed and world > 1 and args.gather_stripes > 0:
         # configs[3]'s survivor gather on the same ranks, after the headline
-        # is measured: its own buffers, so the local ones go first.
-        del data, parity
-        torch.cuda.synchronize(dev)
-        torch.cuda.empty_cache()
+        # is measured (device_run freed its buffers).
         gather_leg(args, f, k, n, S, emax, world, rank, dev, out)  # emits the line and tears down
         return
+    if rank == 0 and world == 1 and args.extra_legs:
+        # The reference's own per-message path (configs[0]) and the wide code
+        # (configs[4]) at N = 1: reported beside the headline, never in value.
+        del f
+        torch.cuda.empty_cache()
+        out["config1"] = guarded_leg(lambda: config1_leg(local, args.config1_reps))
+        out["config5"] = guarded_leg(lambda: config5_leg(local, dev, args.config5_stripes, args.config5_steps,
+                                                         args.config5_warmup))
     if rank == 0:
         emit(out)
     if distributed:
         torch.distributed.destroy_process_group()
 
 
+def gather_what(backend: str) -> str:
+    """What the N > 1 gather leg does, naming the backend that moved the
+    survivors (RCCL on the driver's runs, gloo in a rehearsal)."""
+    how = ("RCCL (batch_isend_irecv = ncclGroupStart/ncclSend/ncclRecv/ncclGroupEnd over xGMI)"
+           if backend == "nccl" else
+           f"{backend} (rehearsal: device rows staged through host memory, ranks sharing GPUs)")
+    return ("shard i of every stripe on rank i mod N; each owner gathers exactly Rebuild's survivors over "
+            + how + " and reconstructs from the receive buffers (rs_reconstruct_ptrs); not part of value")
+
+
+class OnceLine:
+    """Rank 0's JSON line, printed exactly once: by the gather leg when it
+    finishes, or by its watchdog when it does not.  finish() returns True to
+    the one caller that printed it."""
+
+    def __init__(self, rank, out):
+        import threading
+        self.lock = threading.Lock()
+        self.emitted = False
+        self.rank, self.out = rank, out
+
+    def finish(self, gather) -> bool:
+        with self.lock:
+            if self.emitted:
+                return False
+            self.emitted = True
+        if self.rank == 0 and self.out is not None:
+            self.out["gather"] = gather
+            emit(self.out)
+        return True
+
+
+def make_abandon(line: OnceLine, timeout: float, exit_fn=None):
+    """The watchdog's action: print the headline line with the gather leg
+    marked abandoned, then end the process with EXIT_GATHER_ABANDONED (a
+    collective that never completed is a failed run even though the
+    headline was measured).  os._exit: the stuck collective's threads
+    cannot be joined."""
+    exit_fn = exit_fn or os._exit
+
+    def abandon():
+        if line.finish({"status": f"abandoned after {timeout:.0f} s (collective did not complete)"}):
+            sys.stderr.write("bench.py: gather leg abandoned\n")
+            sys.stderr.flush()
+            exit_fn(EXIT_GATHER_ABANDONED)
+    return abandon
+
+
 def gather_leg(args, f, k, n, S, emax, world, rank, dev, out):
     """N > 1: a short shard-distributed leg (sharded_run with
     --gather-stripes owned stripes per rank, 1 warm-up + 2 timed steps,
-    every step checked on a sample) reported as out["gather"].  A watchdog
-    per rank abandons a leg stuck in a collective after --gather-timeout
-    seconds: rank 0 still prints the headline line (gather.status says
-    what happened) and every rank exits, so the headline measurement is
-    never lost to the extra leg.  Wrong shards exit non-zero after the
+    each timed step's output checked on a sample) reported as
+    out["gather"].  A watchdog per rank abandons a leg stuck in a collective
+    after --gather-timeout seconds: rank 0 still prints the headline line
+    (gather.status says what happened) and every rank exits with
+    EXIT_GATHER_ABANDONED, so the headline measurement is kept but the run
+    is not reported as a success.  Wrong shards exit non-zero after the
     line is printed."""
     import threading
 
-    lock = threading.Lock()
-    state = {"emitted": False}
-
-    def finish(gather):
-        with lock:
-            if state["emitted"]:
-                return False
-            state["emitted"] = True
-        if rank == 0 and out is not None:
-            out["gather"] = gather
-            emit(out)
-        return True
-
-    def abandon():
-        if finish({"status": f"abandoned after {args.gather_timeout:.0f} s (collective did not complete)"}):
-            sys.stderr.write("bench.py: gather leg abandoned\n")
-            sys.stderr.flush()
-            os._exit(0)
-
+    line = OnceLine(rank, out)
     torch.distributed.barrier()  # rank 0's CPU baseline is done: start every clock together
-    timer = threading.Timer(args.gather_timeout, abandon)
+    timer = threading.Timer(args.gather_timeout, make_abandon(line, args.gather_timeout))
     timer.daemon = True
     timer.start()
     steps, warmup = 2, 1
-    gather = {"status": "ok", "owned_stripes_per_rank": args.gather_stripes, "shard_bytes": S,
-              "steps": steps, "warmup": warmup,
-              "what": "shard i of every stripe on rank i mod N; each owner gathers exactly Rebuild's "
-                      "survivors over RCCL (batch_isend_irecv) and reconstructs from the receive buffers "
-                      "(rs_reconstruct_ptrs); not part of value"}
+    backend = os.environ.get("RSMI_BENCH_BACKEND", "nccl")
+    gather = {"status": "ok", "backend": backend, "owned_stripes_per_rank": args.gather_stripes,
+              "shard_bytes": S, "steps": steps, "warmup": warmup, "what": gather_what(backend)}
     bad = 0
     try:
         res = sharded_run(f, k, n, S, args.gather_stripes, steps, warmup, args.emin, emax, 0, args.chunks,
@@ -549,9 +775,11 @@ def gather_leg(args, f, k, n, S, emax, world, rank, dev, out):
     except Exception as e:  # reported; the headline line is still printed
         gather["status"] = f"error: {type(e).__name__}: {e}"
     timer.cancel()
-    finish(gather)
+    line.finish(gather)
     if bad:
         raise SystemExit("bench.py: the gather leg reconstructed wrong shards")
+    if gather["status"].startswith("error"):
+        raise SystemExit("bench.py: the gather leg failed: " + gather["status"])
 
 
 def stream_main(args, world, rank, local, dev, distributed):
@@ -630,17 +858,31 @@ def stream_main(args, world, rank, local, dev, distributed):
         torch.distributed.destroy_process_group()
 
 
+def agree_max(value: int, distributed: bool, dev) -> int:
+    """max over ranks of an integer (identity without a process group)."""
+    if not distributed:
+        return value
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.int64, device=stats_device(dev))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t[0])
+
+
 def sharded_run(f, k, n, S, stripes, steps, warmup, emin, emax, pool, chunks, world, rank, dev, distributed,
-                budget_exit=True):
+                budget_exit=True, outs=2):
     """configs[3], shard-distributed placement: shard i of every stripe is
     held by rank i mod N (the p2p analogue of main.go:207 broadcasting each
     shard to peers).  One step = the survivor gather (exactly the survivors
     each owner reads, rsmi/distributed.py) in `chunks` chunks, chunk c + 1's
-    RCCL exchange (communication stream) overlapping chunk c's
+    exchange (communication stream) overlapping chunk c's
     rs_reconstruct_ptrs (compute stream), which reads survivors where they
-    landed.  The per-rank HBM budget is computed before anything is
-    allocated; a budget over the free HBM raises the chunk count, and past
-    64 chunks exits non-zero with the numbers (budget_exit) or returns None.
+    landed; steps are queued back to back with no host sync.  The per-rank
+    HBM budget is computed before anything is allocated; a budget over the
+    free HBM raises the chunk count (agreed over ranks: the max), and past
+    64 chunks every rank exits non-zero with the numbers (budget_exit) or
+    returns None.  Step i writes output buffer i mod `outs`, so the last
+    `outs` timed steps' outputs (the last step and the one before it, whose
+    receive slots the last step reused) are checked on a sample afterwards.
     Every rank returns the all-gathered per-rank statistics and the summary."""
     from rsmi import distributed as rd
 
@@ -655,19 +897,35 @@ def sharded_run(f, k, n, S, stripes, steps, warmup, emin, emax, pool, chunks, wo
     free_b, _ = torch.cuda.mem_get_info(dev)
     if os.environ.get("RSMI_BENCH_BACKEND", "nccl") != "nccl":
         free_b //= -(-world // max(torch.cuda.device_count(), 1))  # ranks share the rehearsal GPU(s)
+    outs = max(1, min(outs, steps))
+    headroom = 4 << 30
+
+    def plan_all(c):
+        tp = time.perf_counter()
+        ps = [rd.plan_exchange(er, k, n, rank, world, S, chunks=c) for er in ersets]
+        return ps, (time.perf_counter() - tp) * 1e3 / len(ersets)
+
     chunks = max(1, chunks)
     while True:
-        tp = time.perf_counter()
-        plans = [rd.plan_exchange(er, k, n, rank, world, S, chunks=chunks) for er in ersets]
-        plan_ms = (time.perf_counter() - tp) * 1e3 / len(ersets)
-        budget = rd.hbm_budget(gstripes, len(ids), S, plans, n, k=k)
-        if budget["total"] * 1e9 <= free_b - (4 << 30) or chunks >= 64:
+        plans, plan_ms = plan_all(chunks)
+        budget = rd.hbm_budget(gstripes, len(ids), S, plans, n, k=k, outs=outs)
+        if budget["total"] * 1e9 <= free_b - headroom or chunks >= 64:
             break
         chunks *= 2
-    if budget["total"] * 1e9 > free_b - (4 << 30):
-        sys.stderr.write(f"bench.py: sharded placement needs {budget['total']:.1f} GB per rank "
+    # Every rank must plan with the same chunk count (plan_exchange pairs
+    # rank p's send segments with rank o's receive slots), and either every
+    # rank runs or none does: two collectives, made by every rank.
+    agreed = agree_max(chunks, distributed, dev)
+    if agreed != chunks:
+        chunks = agreed
+        plans, plan_ms = plan_all(chunks)
+        budget = rd.hbm_budget(gstripes, len(ids), S, plans, n, k=k, outs=outs)
+    fits = not agree_max(int(budget["total"] * 1e9 > free_b - headroom), distributed, dev)
+    if not fits:
+        sys.stderr.write(f"bench.py: sharded placement needs {budget['total']:.1f} GB on rank {rank} "
                          f"({', '.join(f'{key} {v:.1f}' for key, v in budget.items() if key != 'total')}) "
-                         f"but {free_b / 1e9:.1f} GB are free: lower --stripes\n")
+                         f"with {free_b / 1e9:.1f} GB free, or another rank's budget does not fit: "
+                         "lower --stripes\n")
         if budget_exit:
             raise SystemExit(3)
         return None
@@ -691,15 +949,17 @@ def sharded_run(f, k, n, S, stripes, steps, warmup, emin, emax, pool, chunks, wo
     del tmp_d, tmp_p
     if pattern_total(n, emax) <= (1 << 20):
         f.prepare_patterns(emax, sh)
-    bufs = rd.make_buffers(plans, S, dev)
-    tables = [torch.from_numpy(rd.shard_table(p, held, bufs)).to(dev) for p in plans]
+    bufs = rd.make_buffers(plans, S, dev, outs=outs)
+    tables = [torch.from_numpy(rd.shard_table(p, held, bufs, out=i % outs)).to(dev) for i, p in enumerate(plans)]
     er_owned = [np.ascontiguousarray(er[p.owned]) for er, p in zip(ersets, plans)]
     torch.cuda.synchronize(dev)
     rccl = distributed and os.environ.get("RSMI_BENCH_BACKEND", "nccl") == "nccl"
-    comm = torch.cuda.Stream(dev) if rccl else None
+    # The exchange runs on its own stream under either backend (under gloo
+    # the device rows are staged through host memory on that stream).
+    comm = torch.cuda.Stream(dev) if distributed else None
 
     def step(i):
-        rd.run_step(f, held, plans[i], bufs, tables[i], er_owned[i], S, stream, comm)
+        return rd.run_step(f, held, plans[i], bufs, tables[i], er_owned[i], S, stream, comm)
 
     for i in range(warmup):
         step(i)
@@ -708,32 +968,38 @@ def sharded_run(f, k, n, S, stripes, steps, warmup, emin, emax, pool, chunks, wo
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(warmup, warmup + steps):
-        step(i)
+    evs = [step(i) for i in range(warmup, warmup + steps)]
     torch.cuda.synchronize(dev)
     if distributed:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    rec_ms = [a.elapsed_time(b) for a, b in evs if a is not None]
+    rec_ms = sum(rec_ms) / len(rec_ms) if rec_ms else 0.0
     rec_bytes = sum(int(((k + ersets[i][plans[i].owned].sum(axis=1)) * S).sum())
                     for i in range(warmup, warmup + steps))
     xgmi_bytes = sum(plans[i].bytes_in for i in range(warmup, warmup + steps))
-    # Check (untimed) the last step's outputs on a sample of owned stripes:
-    # each stripe regenerated from the global stream and encoded here, its
-    # erased shards compared with what the gather + reconstruct produced.
-    last = plans[-1]
-    sample = np.unique(np.linspace(0, len(last.owned) - 1, num=min(16, len(last.owned))).astype(np.int64))
+    # Check (untimed) the outputs of the last `outs` timed steps on a sample
+    # of owned stripes: each stripe regenerated from the global stream and
+    # encoded here, its erased shards compared with what the gather +
+    # reconstruct wrote into that step's output buffer.
     chk_d = torch.empty(k * S, dtype=torch.uint8, device=dev)
     chk_p = torch.empty(m * S, dtype=torch.uint8, device=dev)
-    bad = 0
-    for j in sample:
-        gs = int(last.owned[j])
-        f.fill_splitmix(chk_d.data_ptr(), k * S, (0x5EED + gs * k * S // 8 * gamma) & (2**64 - 1), sh)
-        f.encode_stripes(chk_d.data_ptr(), k * S, chk_p.data_ptr(), m * S, S, S, 1, sh)
-        full = torch.cat([chk_d.view(k, S), chk_p.view(m, S)])
-        for i in np.nonzero(ersets[-1][gs])[0]:
-            bad += int(not torch.equal(bufs.out[int(last.row[j, i])], full[i]))
+    bad = checked = 0
+    checked_steps = list(range(warmup + steps - outs, warmup + steps))
+    for si in checked_steps:
+        pl = plans[si]
+        out_buf = bufs.outs[si % outs]
+        sample = np.unique(np.linspace(0, len(pl.owned) - 1, num=min(16, len(pl.owned))).astype(np.int64))
+        for j in sample:
+            gs = int(pl.owned[j])
+            f.fill_splitmix(chk_d.data_ptr(), k * S, (0x5EED + gs * k * S // 8 * gamma) & (2**64 - 1), sh)
+            f.encode_stripes(chk_d.data_ptr(), k * S, chk_p.data_ptr(), m * S, S, S, 1, sh)
+            full = torch.cat([chk_d.view(k, S), chk_p.view(m, S)])
+            for i in np.nonzero(ersets[si][gs])[0]:
+                bad += int(not torch.equal(out_buf[int(pl.row[j, i])], full[i]))
+            checked += 1
     torch.cuda.synchronize(dev)
-    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, budget["total"], plan_ms, len(sample), bad],
+    mine = torch.tensor([elapsed, rec_bytes, xgmi_bytes, budget["total"], plan_ms, checked, bad, rec_ms],
                         dtype=torch.float64, device=stats_device(dev))
     if distributed:
         gathered = [torch.zeros_like(mine) for _ in range(world)]
@@ -747,10 +1013,14 @@ def sharded_run(f, k, n, S, stripes, steps, warmup, emin, emax, pool, chunks, wo
     elapsed = max(r[0] for r in per_rank)
     return {"per_rank": per_rank, "elapsed": elapsed, "rec_total": sum(r[1] for r in per_rank),
             "xgmi_total": sum(r[2] for r in per_rank), "chunks": len(plans[0].chunks), "budget": budget,
-            "free_b": free_b, "plan_ms": plan_ms, "rccl": rccl,
+            "free_b": free_b, "plan_ms": plan_ms, "rccl": rccl, "comm_stream": comm is not None,
+            "backend": os.environ.get("RSMI_BENCH_BACKEND", "nccl") if distributed else "none",
             "verified": {"stripes": int(sum(r[5] for r in per_rank)),
                          "mismatched_shards": int(sum(r[6] for r in per_rank)),
-                         "how": "last step, up to 16 owned stripes per rank regenerated and encoded locally"}}
+                         "steps": [s - warmup for s in checked_steps],
+                         "how": f"the last {outs} timed steps (own output buffers; the last step reused the "
+                                "previous one's receive slots), up to 16 owned stripes per rank per step "
+                                "regenerated and encoded locally"}}
 
 
 def gather_summary(res, steps, world):
@@ -764,11 +1034,14 @@ def gather_summary(res, steps, world):
                  "achieved_GBps_total": round(xg, 1), "per_rank_GBps": round(xg / max(world, 1), 1),
                  "link_peak_GBps": 153.0, "links_per_gpu": 7},
         "chunks": res["chunks"],
-        "overlap": "RCCL exchange of chunk c+1 on a communication stream || reconstruct of chunk c"
-                   if res["rccl"] else "none (gloo rehearsal: chunks in sequence)",
+        "overlap": ("RCCL" if res["rccl"] else res.get("backend", "gloo") + " (host-staged)")
+                   + " exchange of chunk c+1 on a communication stream || reconstruct of chunk c"
+                   if res.get("comm_stream", res["rccl"]) else "none (chunks in sequence)",
         "hbm_budget_GB": {key: round(v, 2) for key, v in res["budget"].items()},
         "hbm_free_GB": round(res["free_b"] / 1e9, 1),
         "plan_ms_per_step": round(res["plan_ms"], 2),
+        "reconstruct_stream_ms_per_step": round(max(r[7] for r in res["per_rank"]), 3)
+        if len(res["per_rank"][0]) > 7 else None,
         "verified": res["verified"],
         "per_rank": [{"rank": r, "ms_per_step": round(v[0] / steps * 1e3, 3),
                       "gathered_GB_per_step": round(v[2] / steps / 1e9, 3),

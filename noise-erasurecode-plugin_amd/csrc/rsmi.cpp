@@ -211,6 +211,13 @@ struct Lease {
     std::vector<uint32_t> pid, start;          // reconstruct scratch
     std::vector<uint64_t> sort_a, sort_b;      // (bucket, stripe) radix-sort scratch
     std::vector<PatKey> miss_keys;             // distinct new patterns of a call
+    // The pattern rows this lease's launches are known to be ordered after:
+    // ids below seen_uploaded of table generation seen_tables (launch_reconstruct
+    // waits for pat_ev only for a pattern built since, or after the tables
+    // moved -- growth or eviction -- so a caller whose patterns are all old
+    // never queues behind another caller's build).
+    size_t seen_uploaded = 0;
+    uint64_t seen_tables = ~uint64_t(0);
 
     bool init() {
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
@@ -286,6 +293,7 @@ struct rs_ctx {
     size_t pat_cap = 0;     // soft bound; reaching it evicts the whole cache
     int test_fail_flush = 0, flush_attempts = 0;  // RSMI_TEST_FAIL_FLUSH (tests)
     uint64_t evictions = 0;
+    uint64_t tables_gen = 0;  // bumped when the device tables move (growth) or are rebuilt (eviction)
     std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
     std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
     hipEvent_t pat_ev = nullptr;
@@ -599,6 +607,7 @@ void evict_patterns(rs_ctx* c) {
     c->h_mask.clear();
     c->uploaded = 0;
     ++c->evictions;
+    ++c->tables_gen;
 }
 
 // Undoes the patterns created since the last successful build (pat_mu
@@ -625,6 +634,26 @@ void wait_patterns(rs_ctx* c, hipStream_t s) {
     if (c->pat_ev_valid) (void)hipStreamWaitEvent(s, c->pat_ev, 0);
 }
 
+// launch_reconstruct's wait (pat_mu held; L.begin(s) already queued): only
+// when a pattern the launch reads -- ids up to max_pid -- was built after
+// the lease's last wait, or the tables moved since.  Otherwise the rows are
+// complete before the lease's previous launch, which s follows through
+// L.begin.  With build_after_caller, pat_ev also covers the building
+// caller's queued work; an unconditional wait would put every concurrent
+// caller behind that backlog.
+// Returns whether it waited; the caller commits the lease's watermark
+// (seen_patterns) only after L.end(s), so a failed launch leaves no claim.
+bool wait_patterns_for(rs_ctx* c, Lease& L, size_t max_pid, hipStream_t s) {
+    if (L.seen_tables == c->tables_gen && max_pid < L.seen_uploaded) return false;
+    wait_patterns(c, s);
+    return true;
+}
+
+void seen_patterns(const rs_ctx* c, Lease& L) {
+    L.seen_tables = c->tables_gen;
+    L.seen_uploaded = c->uploaded;
+}
+
 // Uploads the keys of the patterns created since the last flush and builds
 // them on the GPU (one workgroup per pattern: survivor and erased-id rows
 // from the key, then the decode rows), pat_mu exclusive.  Builds run on the
@@ -642,8 +671,10 @@ int flush_patterns_impl(rs_ctx* c, hipStream_t caller, bool has_caller) {
     // Growth frees the outgrown tables on the build stream: order it after
     // every launch that may still read them first.
     if (c->d_pcoef.needs(npat * m * k) || c->d_psrc.needs(npat * k * 4) || c->d_pdst.needs(npat * ds * 4) ||
-        c->d_pcnt.needs(npat * 4) || c->d_pstat.needs(npat * 4))
+        c->d_pcnt.needs(npat * 4) || c->d_pstat.needs(npat * 4)) {
         order_after_readers(c);
+        ++c->tables_gen;  // old rows are copied into the new tables on the build stream
+    }
     if (!c->d_pcoef.reserve_keep(npat * m * k, first * m * k, s) ||
         !c->d_psrc.reserve_keep(npat * k * 4, first * k * 4, s) ||
         !c->d_pdst.reserve_keep(npat * ds * 4, first * ds * 4, s) ||
@@ -750,11 +781,12 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     auto bucket = [&](size_t i) -> size_t { return kernel_of(pid[i]) * npat + (no_sort ? 0 : pid[i]); };
     size_t count[8] = {};  // stripes per kernel (nk <= 6)
     int max_lo = 0;
-    size_t used = 0;
+    size_t used = 0, max_pid = 0;
     for (size_t i = 0; i < stripes; ++i) {
         const uint32_t p = pid[i];
         if (!c->h_cnt[p]) continue;  // stripes with nothing erased are skipped
         ++used;
+        max_pid = std::max<size_t>(max_pid, p);
         const size_t kk = kernel_of(p);
         ++count[kk];
         if (kk == 0) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
@@ -803,7 +835,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         for (size_t j = 0; j < keys.size(); ++j) put(j, static_cast<size_t>(keys[j] & 0xFFFFFFFFu));
     }
     L.begin(s);  // the descriptor buffer's previous readers
-    wait_patterns(c, s);
+    const bool waited = wait_patterns_for(c, L, max_pid, s);
     if (!L.d_stripe_pat.reserve_on(desc_bytes, s)) return RS_ENOMEM;
     hipError_t e = hipMemcpyAsync(L.d_stripe_pat.p, desc, desc_bytes, hipMemcpyHostToDevice, s);
     L.st_stripe.release_after(s);
@@ -847,6 +879,7 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         e = kk <= static_cast<size_t>(T) ? c->bitslice->rec_top_launch[kk - 1](b, s) : c->bitslice->reconstruct(b, s);
     }
     L.end(s);  // under pat_mu: an eviction waits for these launches
+    if (waited && e == hipSuccess) seen_patterns(c, L);
     return hip_status(e);
 }
 

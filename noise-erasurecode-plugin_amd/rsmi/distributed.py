@@ -39,7 +39,7 @@ Shard messages arrived).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -245,11 +245,12 @@ def plan_exchange(erased: np.ndarray, k: int, n: int, rank: int, world: int, sha
 
 # -------------------------------------------------------------- memory ----
 def hbm_budget(gstripes: int, nloc: int, shard_bytes: int, plans: Sequence[ExchangePlan], n: int,
-               slots: int = 2, setup_batch: int = 64, k: int = 0) -> Dict[str, float]:
+               slots: int = 2, setup_batch: int = 64, k: int = 0, outs: int = 1) -> Dict[str, float]:
     """Per-rank device bytes of the shard-distributed step (GB), computed
     before anything is allocated: the holder buffer, the send / receive
-    slots (sized by the largest chunk of any step), the output buffer (the
-    largest step), the shard tables and the setup batch."""
+    slots (sized by the largest chunk of any step), the `outs` output
+    buffers (each sized by the largest step), the shard tables and the setup
+    batch."""
     S = shard_bytes
     send = max((c.n_send for p in plans for c in p.chunks), default=0)
     recv = max((c.n_recv for p in plans for c in p.chunks), default=0)
@@ -260,7 +261,7 @@ def hbm_budget(gstripes: int, nloc: int, shard_bytes: int, plans: Sequence[Excha
         "held": gstripes * nloc * S,
         "send": nslots * max(send, 1) * S,
         "recv": nslots * max(recv, 1) * S,
-        "out": max(out, 1) * S,
+        "out": max(1, outs) * max(out, 1) * S,
         "tables": owned * n * 8 * 2,
         "setup": setup_batch * max(k, 1) * S * 2,
     }
@@ -273,20 +274,38 @@ def hbm_budget(gstripes: int, nloc: int, shard_bytes: int, plans: Sequence[Excha
 class GatherBuffers:
     """Reusable per-rank buffers of the exchange (allocate once, pass to
     every step): `slots` send and receive buffers [rows, S] (chunk c uses
-    slot c mod slots) and the output buffer [rows, S]."""
+    slot c mod slots) and a ring of output buffers [rows, S] (step i of a
+    run writes outs[i mod len(outs)], so the last len(outs) steps' outputs
+    survive the run and can be checked).
+
+    slot_free[s] is the compute-stream event after the last reconstruct that
+    read receive slot s (None: free).  It is carried from step to step:
+    the next exchange into slot s -- in this step or the next one -- waits
+    for it on the communication stream, so a receive never overwrites
+    survivors a queued reconstruct has yet to read."""
     send: List[object]
     recv: List[object]
-    out: object
+    outs: List[object]
+    slot_free: List[object] = field(default_factory=list)
+
+    def __post_init__(self):
+        if not self.slot_free:
+            self.slot_free = [None] * len(self.recv)
 
     @property
     def slots(self) -> int:
         return len(self.recv)
 
+    @property
+    def out(self):
+        return self.outs[0]
 
-def make_buffers(plans: Sequence[ExchangePlan], shard_bytes: int, device, slots: int = 2) -> GatherBuffers:
-    """Buffers sized for the largest chunk and the largest step of `plans`.
-    Shard rows must stay 16-byte aligned for the engine's vector loads, so
-    shard_bytes must be a multiple of 16."""
+
+def make_buffers(plans: Sequence[ExchangePlan], shard_bytes: int, device, slots: int = 2,
+                 outs: int = 1) -> GatherBuffers:
+    """Buffers sized for the largest chunk and the largest step of `plans`,
+    with `outs` output buffers.  Shard rows must stay 16-byte aligned for
+    the engine's vector loads, so shard_bytes must be a multiple of 16."""
     import torch
     if shard_bytes % 16:
         raise ValueError(f"shard_bytes {shard_bytes} is not a multiple of 16 (the kernels load 16-byte vectors)")
@@ -294,14 +313,15 @@ def make_buffers(plans: Sequence[ExchangePlan], shard_bytes: int, device, slots:
     mk = lambda rows: torch.empty((max(rows, 1), shard_bytes), dtype=torch.uint8, device=device)
     send = max(c.n_send for p in plans for c in p.chunks)
     recv = max(c.n_recv for p in plans for c in p.chunks)
+    n_out = max(p.n_out for p in plans)
     return GatherBuffers([mk(send) for _ in range(nslots)], [mk(recv) for _ in range(nslots)],
-                         mk(max(p.n_out for p in plans)))
+                         [mk(n_out) for _ in range(max(1, outs))])
 
 
-def shard_table(plan: ExchangePlan, held, bufs: GatherBuffers) -> np.ndarray:
+def shard_table(plan: ExchangePlan, held, bufs: GatherBuffers, out: int = 0) -> np.ndarray:
     """[owned, n] int64 device addresses for rs_reconstruct_ptrs: every
     survivor where it lies (its chunk's receive slot for REMOTE), every
-    erased shard at its output row."""
+    erased shard at its row of output buffer `out`."""
     S = held.shape[-1]
     if S % 16:
         raise ValueError(f"shard bytes {S} is not a multiple of 16")
@@ -309,7 +329,7 @@ def shard_table(plan: ExchangePlan, held, bufs: GatherBuffers) -> np.ndarray:
     m = plan.kind == LOCAL
     t[m] = held.data_ptr() + plan.row[m] * S
     m = plan.kind == OUTPUT
-    t[m] = bufs.out.data_ptr() + plan.row[m] * S
+    t[m] = bufs.outs[out].data_ptr() + plan.row[m] * S
     t[plan.kind == UNUSED] = held.data_ptr()
     for c, ch in enumerate(plan.chunks):
         blk = slice(ch.lo, ch.hi)
@@ -367,8 +387,8 @@ def gather_survivors(held, plan: ExchangePlan, bufs: GatherBuffers, group=None, 
 def reconstruct_owned(fec, plan: ExchangePlan, table_dev, erased_owned: np.ndarray, shard_bytes: int,
                       stream: int = 0, chunk: Optional[int] = None) -> None:
     """Regenerates the erased shards of the owned stripes (all, or one
-    chunk's) into bufs.out through the shard table (a device int64 tensor
-    from shard_table)."""
+    chunk's) into the output buffer the shard table (a device int64 tensor
+    from shard_table) points at."""
     n = plan.kind.shape[1]
     lo, hi = (0, len(plan.owned)) if chunk is None else (plan.chunks[chunk].lo, plan.chunks[chunk].hi)
     if hi <= lo:
@@ -380,21 +400,30 @@ def reconstruct_owned(fec, plan: ExchangePlan, table_dev, erased_owned: np.ndarr
 def run_step(fec, held, plan: ExchangePlan, bufs: GatherBuffers, table_dev, erased_owned: np.ndarray,
              shard_bytes: int, compute_stream, comm_stream=None, group=None):
     """One pipelined step: chunk c's exchange on comm_stream, its
-    reconstruct on compute_stream after the exchange's event; chunk c's
-    slot is reused by chunk c + slots only after chunk c's reconstruct.
-    Without a comm stream (gloo) the chunks run one after the other.
-    Returns the compute stream's events bracketing the step's reconstructs
-    (first start, last end) for timing."""
+    reconstruct on compute_stream after the exchange's event.  Before an
+    exchange lands in receive slot s, comm_stream waits for bufs.slot_free[s]
+    -- the reconstruct that last read slot s, in this step or in the step
+    before (steps are queued back to back with no host sync, so without the
+    carried event step i + 1's first receives would overwrite survivors that
+    step i's last reconstructs still read).  Without a comm stream the
+    chunks run one after the other on the current stream.
+
+    Returns (start, end): compute-stream events recorded before the step's
+    first reconstruct is queued and after its last one (None, None without a
+    comm stream)."""
     import torch
     slots = bufs.slots
-    rec_done = [None] * len(plan.chunks)
-    for c in range(len(plan.chunks)):
-        if comm_stream is None:
+    if comm_stream is None:
+        for c in range(len(plan.chunks)):
             gather_survivors(held, plan, bufs, group, c)
             reconstruct_owned(fec, plan, table_dev, erased_owned, shard_bytes, compute_stream.cuda_stream, c)
-            continue
-        if c >= slots and rec_done[c - slots] is not None:
-            comm_stream.wait_event(rec_done[c - slots])
+        return None, None
+    start = torch.cuda.Event(enable_timing=True)
+    start.record(compute_stream)
+    for c in range(len(plan.chunks)):
+        slot = c % slots
+        if bufs.slot_free[slot] is not None:
+            comm_stream.wait_event(bufs.slot_free[slot])
         with torch.cuda.stream(comm_stream):
             gather_survivors(held, plan, bufs, group, c)
             got = torch.cuda.Event()
@@ -403,9 +432,10 @@ def run_step(fec, held, plan: ExchangePlan, bufs: GatherBuffers, table_dev, eras
         reconstruct_owned(fec, plan, table_dev, erased_owned, shard_bytes, compute_stream.cuda_stream, c)
         ev = torch.cuda.Event()
         ev.record(compute_stream)
-        rec_done[c] = ev
-    if comm_stream is not None:
-        compute_stream.wait_stream(comm_stream)
+        bufs.slot_free[slot] = ev
+    end = torch.cuda.Event(enable_timing=True)
+    end.record(compute_stream)
+    return start, end
 
 
 def shard_bytes_at(plan: ExchangePlan, held, bufs: GatherBuffers, j: int, i: int):

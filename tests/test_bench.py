@@ -137,3 +137,107 @@ def test_gather_flags_pass_through_the_launcher():
     argv = ["--gpus", "8", "--gather-stripes", "256", "--gather-timeout", "60"]
     cmd = bench.launch_command(8, argv, 29500)
     assert cmd[-len(argv):] == argv and "--nproc-per-node=8" in cmd
+
+
+def test_job_totals_sum_each_ranks_own_bytes():
+    """value = every rank's own algorithmic bytes summed over the slowest
+    rank's time (ranks draw their own erasure sets, so their reconstruct
+    bytes differ: rank 0's bytes x world would be wrong)."""
+    per_rank = [[2.0, 1.0, 1.0, 100.0], [2.5, 1.0, 1.0, 130.0], [1.5, 1.0, 1.0, 90.0]]
+    secs, total = bench.job_totals(per_rank)
+    assert secs == 2.5 and total == 320.0
+    assert bench.job_totals([[1.0, 7.0]]) == (1.0, 7.0)
+
+
+def test_gather_watchdog_prints_once_then_exits_nonzero(monkeypatch):
+    """An abandoned gather leg prints the headline line (gather.status says
+    what happened) and ends the process with EXIT_GATHER_ABANDONED, never 0;
+    a leg that finished first keeps the watchdog from printing again or
+    exiting."""
+    lines = []
+    monkeypatch.setattr(bench, "emit", lambda obj: lines.append(dict(obj)))
+    codes = []
+    line = bench.OnceLine(0, {"metric": "m", "value": 1.0})
+    bench.make_abandon(line, 5.0, exit_fn=codes.append)()
+    assert codes == [bench.EXIT_GATHER_ABANDONED] and bench.EXIT_GATHER_ABANDONED != 0
+    assert len(lines) == 1 and lines[0]["gather"]["status"].startswith("abandoned after 5 s")
+    bench.make_abandon(line, 5.0, exit_fn=codes.append)()  # second firing: nothing
+    assert codes == [bench.EXIT_GATHER_ABANDONED] and len(lines) == 1
+    done = bench.OnceLine(0, {"metric": "m"})
+    assert done.finish({"status": "ok"})
+    bench.make_abandon(done, 5.0, exit_fn=codes.append)()
+    assert codes == [bench.EXIT_GATHER_ABANDONED] and len(lines) == 2
+    other = bench.OnceLine(1, {"metric": "m"})  # rank 1 prints nothing but still exits non-zero
+    bench.make_abandon(other, 5.0, exit_fn=codes.append)()
+    assert codes[-1] == bench.EXIT_GATHER_ABANDONED and len(lines) == 2
+
+
+def test_gather_what_names_the_backend():
+    assert "RCCL" in bench.gather_what("nccl") and "gloo" not in bench.gather_what("nccl")
+    g = bench.gather_what("gloo")
+    assert "gloo" in g and "RCCL" not in g
+
+
+def test_gather_summary_overlap_names_the_backend():
+    per_rank = [[2.0, 40e9, 10e9, 12.5, 1.0, 16, 0, 3.0]]
+    res = {"per_rank": per_rank, "elapsed": 2.0, "rec_total": 40e9, "xgmi_total": 10e9, "chunks": 2,
+           "budget": {"total": 1.0}, "free_b": 1e9, "plan_ms": 0.5, "rccl": False, "comm_stream": True,
+           "backend": "gloo", "verified": {"stripes": 16, "mismatched_shards": 0, "how": "x"}}
+    g = bench.gather_summary(res, 2, 1)
+    assert g["overlap"].startswith("gloo (host-staged) exchange") and g["reconstruct_stream_ms_per_step"] == 3.0
+    res["rccl"], res["backend"] = True, "nccl"
+    assert bench.gather_summary(res, 2, 1)["overlap"].startswith("RCCL exchange")
+
+
+def test_agree_max_without_a_process_group():
+    assert bench.agree_max(8, False, None) == 8
+
+
+def test_extra_leg_flags(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert a.extra_legs and a.config5_stripes == 16384 and a.config1_reps > 0
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--no-extra-legs", "--config5-stripes", "64"])
+    a = bench.parse()
+    assert not a.extra_legs and a.config5_stripes == 64
+
+
+def test_guarded_leg_reports_failures():
+    assert bench.guarded_leg(lambda: {"status": "ok"}) == {"status": "ok"}
+    r = bench.guarded_leg(lambda: 1 / 0)
+    assert r["status"].startswith("error: ZeroDivisionError")
+
+
+def _agree_worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RSMI_BENCH_BACKEND="gloo")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import torch
+        got = (bench.agree_max([2, 8][rank], True, torch.device("cpu")),
+               bench.agree_max([0, 1][rank], True, torch.device("cpu")))
+        dist.destroy_process_group()
+        q.put((rank, got))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_agree_max_gloo_world2():
+    """Every rank ends with the same chunk count (the max) and the same
+    fits verdict (any rank over budget -> none runs)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: (8, 1), 1: (8, 1)}, res

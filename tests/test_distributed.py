@@ -306,3 +306,91 @@ def test_plan_send_recv_orders_agree():
                 i = p + slot * world
                 j = po.owned.tolist().index(s)
                 assert po.kind[j, i] == rd.REMOTE and po.row[j, i] == po.recv_off[p] + r
+
+
+class _FakeEvent:
+    n = 0
+
+    def __init__(self, enable_timing=False):
+        _FakeEvent.n += 1
+        self.id = _FakeEvent.n
+        self.stream = None
+
+    def record(self, stream):
+        self.stream = stream
+        stream.log.append(("record", stream.name, self.id))
+
+
+class _FakeStream:
+    def __init__(self, name, log):
+        self.name, self.log, self.cuda_stream = name, log, 0
+
+    def wait_event(self, ev):
+        self.log.append(("wait", self.name, ev.id))
+
+
+def test_run_step_orders_slot_reuse_across_steps(monkeypatch):
+    """Back-to-back steps with a communication stream (the RCCL path, no
+    host sync between steps): every exchange into receive slot s after its
+    first use waits for the event recorded after the last reconstruct that
+    read slot s -- including step i + 1's first chunks against step i's
+    last reconstructs (the write-after-read race of round 3)."""
+    import contextlib
+    log = []
+    comm, compute = _FakeStream("comm", log), _FakeStream("compute", log)
+    current = {"s": compute}
+
+    @contextlib.contextmanager
+    def fake_stream(st):
+        prev, current["s"] = current["s"], st
+        yield
+        current["s"] = prev
+
+    monkeypatch.setattr(torch.cuda, "Event", _FakeEvent)
+    monkeypatch.setattr(torch.cuda, "stream", fake_stream)
+    monkeypatch.setattr(rd, "gather_survivors",
+                        lambda held, plan, bufs, group, c: log.append(("gather", current["s"].name, c % bufs.slots)))
+    monkeypatch.setattr(rd, "reconstruct_owned",
+                        lambda fec, plan, table, er, S_, stream, c: log.append(("rec", "compute", c % 2)))
+    _, _, er = dataset()
+    for chunks in (1, 2, 3, 4):
+        log.clear()
+        plan = rd.plan_exchange(er, K, N, 0, 2, S, chunks=chunks)
+        bufs = rd.GatherBuffers([None] * min(2, chunks), [None] * min(2, chunks), [None])
+        for _ in range(3):
+            start, end = rd.run_step(None, None, plan, bufs, None, er, S, compute, comm)
+            assert start is not None and end is not None
+        last_rec_event = {}   # slot -> event recorded after its latest reconstruct
+        waited = set()
+        pending_slot = None
+        for op in log:
+            if op[0] == "wait" and op[1] == "comm":
+                waited.add(op[2])
+            elif op[0] == "gather":
+                assert op[1] == "comm"
+                slot = op[2]
+                if slot in last_rec_event:
+                    assert last_rec_event[slot] in waited, (chunks, op, log)
+            elif op[0] == "rec":
+                pending_slot = op[2] % bufs.slots
+            elif op[0] == "record" and op[1] == "compute" and pending_slot is not None:
+                last_rec_event[pending_slot] = op[2]
+                pending_slot = None
+        assert sum(1 for op in log if op[0] == "gather") == 3 * len(plan.chunks)
+
+
+def test_output_ring_tables_point_at_their_own_buffer():
+    """Step i writes output buffer i mod outs: the tables of two steps
+    differ only in the erased entries, which lie in different buffers."""
+    _, full, er = dataset()
+    held = torch.from_numpy(np.ascontiguousarray(full[:, rd.local_shard_ids(0, N, 1), :]))
+    plan = rd.plan_exchange(er, K, N, 0, 1, S)
+    bufs = rd.make_buffers([plan], S, "cpu", outs=2)
+    assert len(bufs.outs) == 2 and bufs.out is bufs.outs[0]
+    t0, t1 = rd.shard_table(plan, held, bufs, 0), rd.shard_table(plan, held, bufs, 1)
+    out = plan.kind == rd.OUTPUT
+    assert (t0[~out] == t1[~out]).all()
+    assert (t1[out] - t0[out] == bufs.outs[1].data_ptr() - bufs.outs[0].data_ptr()).all()
+    b1 = rd.hbm_budget(STRIPES, 14, S, [plan], N, k=K, outs=1)
+    b2 = rd.hbm_budget(STRIPES, 14, S, [plan], N, k=K, outs=2)
+    assert abs(b2["out"] - 2 * b1["out"]) < 1e-12
