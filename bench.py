@@ -397,8 +397,10 @@ def config1_leg(local, reps=50):
       * codec: rs_encode / rs_decode at the C ABI on caller-owned pageable
         buffers (what the cgo shim hands over; PCIe-inclusive);
       * plugin: the C++ ShardPlugin mirror -- prepareShards into 14 Shard
-        messages (no signer), and 10 Receive calls whose last one decodes
-        (no verifier), through its Python binding;
+        messages (no signer), and the 10 surviving Shards received (pooled:
+        with m = 4 lost the reference's Receive never gets its k+1-th,
+        decode-triggering shard, main.go:65-72) then decoded with
+        FEC.Decode, through its Python binding;
       * cpu: the oracle on 1 thread for the same blob (scalar mul_table and
         AVX2 split-nibble addmul: encode, and Rebuild of the dropped data
         shards).
@@ -453,25 +455,39 @@ def config1_leg(local, reps=50):
         s_.Unmarshal(wires[i])
         msgs.append(s_)
 
+    hf = h.NewFEC(k, n)
+    shares = [h.Share(int(s_.ShardNumber), s_.ShardData) for s_ in msgs]
+
     def receive():
         r = h.NewShardPlugin(None, None, k, n)
-        ev = None
         for s_ in msgs:
-            ev = r.Receive(me, s_)
-        if not ev.decoded or ev.message != blob:
-            raise RuntimeError("config1: Receive did not decode the blob")
+            if not r.Receive(me, s_).pooled:
+                raise RuntimeError("config1: a surviving shard was not pooled")
+        got, _ = hf.Decode(None, shares)
+        if got != blob:
+            raise RuntimeError("config1: the pooled shares did not decode to the blob")
     recv_ms = _median_ms(receive, reps)
-    # the oracle on one thread, same blob
+    # The oracle on one thread, same blob.  Encode: parity only (infectious
+    # emits the data shares as views).  Decode: what Decode does for dst --
+    # the present data shares copied in, the dropped ones regenerated into
+    # their slots (Rebuild) -- like rs_decode.
     cpu = {}
     er = np.zeros((1, n), dtype=np.uint8)
     er[0, [i for i in lost if i < k]] = 1  # Rebuild regenerates the dropped data shares only
     par = np.zeros(m * S, dtype=np.uint8)
+    dst_cpu = np.zeros(L, dtype=np.uint8)
+    present = [i for i in range(k) if i not in lost]
     for name, simd in (("scalar_1t", False), ("avx2_1t", True)):
         e_ms = _median_ms(lambda: oracle.encode_batch(E, k, n, blob_np, S, 1, simd=simd, threads=1, out=par),
                           max(5, reps // 5))
-        work = blob_np.copy()
-        d_ms = _median_ms(lambda: oracle.reconstruct_batch(E, k, n, work, par, S, 1, er, simd=simd, threads=1),
-                          max(5, reps // 5))
+
+        def cpu_dec():
+            for i in present:
+                dst_cpu[i * S:(i + 1) * S] = blob_np[i * S:(i + 1) * S]
+            return oracle.reconstruct_batch(E, k, n, dst_cpu, par, S, 1, er, simd=simd, threads=1)
+        d_ms = _median_ms(cpu_dec, max(5, reps // 5))
+        if not np.array_equal(dst_cpu, blob_np):
+            raise RuntimeError("config1: the oracle's decode did not return the blob")
         cpu[name] = {"encode_ms": e_ms, "decode4_ms": d_ms}
     best = min(cpu.values(), key=lambda v: v["encode_ms"])
     return {
@@ -481,7 +497,7 @@ def config1_leg(local, reps=50):
         "message_bytes": L, "shard_bytes": S, "dropped": lost, "reps": reps,
         "codec": {"encode_ms": enc_ms, "decode4_ms": dec_ms,
                   "encode_GBps": round(L * n / k / enc_ms / 1e6, 2)},
-        "plugin": {"prepareShards_ms": prep_ms, "receive10_decode_ms": recv_ms,
+        "plugin": {"prepareShards_ms": prep_ms, "receive10_then_decode_ms": recv_ms,
                    "note": "C++ ShardPlugin mirror through pybind (blob and 14 shards copied across the "
                            "binding); no signer / verifier"},
         "cpu_1t": cpu,

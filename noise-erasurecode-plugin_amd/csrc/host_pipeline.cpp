@@ -112,13 +112,16 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
 }
 
 // -------------------------------------------------------- HostPipeline ----
-HostPipeline::HostPipeline() : pool_(CopyPool::shared()) {}
+HostPipeline::HostPipeline() : pool_(CopyPool::shared()) {
+    const char* e = std::getenv("RSMI_HOSTPIPE");
+    direct_ = !(e && std::strcmp(e, "dma") == 0);
+}
 
 HostPipeline::~HostPipeline() {
     for (Slot& s : slots_) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
-        if (s.d_in) (void)hipFreeAsync(s.d_in, s.stream);
-        if (s.d_out) (void)hipFreeAsync(s.d_out, s.stream);
+        if (!direct_ && s.d_in) (void)hipFreeAsync(s.d_in, s.stream);
+        if (!direct_ && s.d_out) (void)hipFreeAsync(s.d_out, s.stream);
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.h_in) (void)hipHostFree(s.h_in);
         if (s.h_out) (void)hipHostFree(s.h_out);
@@ -137,6 +140,18 @@ bool HostPipeline::grow(Slot& s, uint8_t** h, uint8_t** d, size_t* cap, size_t b
     const size_t want = std::max(bytes, 2 * *cap);
     uint8_t* nh = nullptr;
     if (hipHostMalloc(reinterpret_cast<void**>(&nh), want, hipHostMallocDefault) != hipSuccess) return false;
+    if (direct_) {
+        // The kernel addresses the staging itself; the outgrown buffer may
+        // still be read by the slot's previous chunk only if it was not
+        // drained, and grow runs after drain.
+        void* alias = nullptr;
+        if (hipHostGetDevicePointer(&alias, nh, 0) != hipSuccess) alias = nh;
+        if (*h) s.retired.push_back(*h);
+        *h = nh;
+        *d = static_cast<uint8_t*>(alias);
+        *cap = want;
+        return true;
+    }
     if (*d && hipFreeAsync(*d, s.stream) != hipSuccess) {
         (void)hipHostFree(nh);
         return false;
@@ -175,8 +190,14 @@ hipError_t HostPipeline::drain(Slot& s, uint8_t* const* dsts, int e) {
 hipError_t HostPipeline::run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e,
                              size_t S, const ChunkLaunch& launch) {
     if (S == 0 || e == 0) return hipSuccess;
-    // Column chunk per shard: about kChunkBytes of survivors per chunk.
-    const size_t cb = round_up(std::min(S, std::max<size_t>(4096, kChunkBytes / k)), 256);
+    // Column chunk per shard: about kChunkBytes of survivors per chunk
+    // (RSMI_HOSTPIPE_CHUNK overrides, for A/B runs).
+    static const size_t chunk_bytes = [] {
+        const char* e = std::getenv("RSMI_HOSTPIPE_CHUNK");
+        const long long v = e ? std::atoll(e) : 0;
+        return v > 0 ? static_cast<size_t>(v) : kChunkBytes;
+    }();
+    const size_t cb = round_up(std::min(S, std::max<size_t>(4096, chunk_bytes / k)), 256);
     const size_t nchunks = (S + cb - 1) / cb;
     hipError_t err = hipSuccess;
     size_t c = 0;
@@ -192,10 +213,14 @@ hipError_t HostPipeline::run(const uint8_t* const* srcs, int k, uint8_t* const* 
         std::vector<CopyPool::Piece> in;
         for (int j = 0; j < k; ++j) in.push_back({s.h_in + j * cb, srcs[j] + c0, w});
         pool_.run(in);
-        err = hipMemcpyAsync(s.d_in, s.h_in, cb * static_cast<size_t>(k), hipMemcpyHostToDevice, s.stream);
-        if (err == hipSuccess) err = launch(s.d_in, s.d_out, cb, w, s.stream);
-        if (err == hipSuccess)
-            err = hipMemcpyAsync(s.h_out, s.d_out, cb * static_cast<size_t>(e), hipMemcpyDeviceToHost, s.stream);
+        if (direct_) {
+            err = launch(s.d_in, s.d_out, cb, w, s.stream);
+        } else {
+            err = hipMemcpyAsync(s.d_in, s.h_in, cb * static_cast<size_t>(k), hipMemcpyHostToDevice, s.stream);
+            if (err == hipSuccess) err = launch(s.d_in, s.d_out, cb, w, s.stream);
+            if (err == hipSuccess)
+                err = hipMemcpyAsync(s.h_out, s.d_out, cb * static_cast<size_t>(e), hipMemcpyDeviceToHost, s.stream);
+        }
         if (err == hipSuccess) err = hipEventRecord(s.done, s.stream);
         if (err == hipSuccess) {
             s.pending = true;

@@ -1,8 +1,10 @@
 // host_pipeline.hpp -- the host-buffer path of the C ABI (rs_encode /
 // rs_decode, i.e. the cgo calls replacing infectious Encode/Decode at
 // main.go:262 / :77): caller bytes are streamed through pinned
-// (hipHostMalloc) staging in column chunks, with each chunk's H2D copy,
-// kernel and D2H copy on one of three HIP streams so that chunk c's GPU work
+// (hipHostMalloc) staging in column chunks.  Each chunk's kernel reads its
+// survivors from the pinned staging and writes its outputs back into it
+// over PCIe (direct mode: no copy-engine transfer, whose setup dominated a
+// 1 MiB message), on one of three HIP streams so that chunk c's GPU work
 // overlaps the staging copies of chunks c-1 and c+1.  Pageable <-> pinned
 // copies are split over a process-wide worker pool.
 //
@@ -80,11 +82,17 @@ public:
     void copy(const std::vector<CopyPool::Piece>& pieces) { pool_.run(pieces); }
 
     static constexpr int kSlots = 3;
+    // Direct mode (default; RSMI_HOSTPIPE=dma selects the copy-engine path):
+    // the kernel codes straight out of / into the pinned staging.
+    bool direct() const { return direct_; }
 
 private:
     struct Slot {
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
+        // d_in / d_out: device buffers (DMA mode) or the device aliases of
+        // h_in / h_out (direct mode: the kernel reads and writes the pinned
+        // staging over PCIe, no copy engine).
         uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
         size_t cap_in = 0, cap_out = 0;
         bool pending = false;
@@ -96,6 +104,7 @@ private:
     hipError_t drain(Slot& s, uint8_t* const* dsts, int e);
     Slot slots_[kSlots];
     CopyPool& pool_;
+    bool direct_ = true;
 };
 
 }  // namespace rsmi

@@ -116,4 +116,54 @@ Status FEC::DecodeBatch(std::vector<std::vector<Share>>& msgs, std::vector<std::
     return rc == RS_OK ? Status::Ok() : from(rc, "DecodeBatch");
 }
 
+Status FEC::DecodeShared(std::vector<uint8_t>* dst, const std::vector<std::shared_ptr<const Share>>& shares) {
+    const int cnt = static_cast<int>(shares.size());
+    const size_t S = cnt ? shares[0]->Data.size() : 0;
+    std::vector<int> nums(cnt);
+    std::vector<const uint8_t*> ptrs(cnt);
+    for (int i = 0; i < cnt; ++i) {
+        if (shares[i]->Data.size() != S) return from(RS_ESHARE_LEN, "Decode");
+        nums[i] = shares[i]->Number;
+        ptrs[i] = shares[i]->Data.data();
+    }
+    std::vector<uint8_t> out(static_cast<size_t>(k_) * S);
+    const int rc = rs_decode(ctx_, nums.data(), ptrs.data(), cnt, S, out.data());
+    if (rc != RS_OK) return from(rc, "Decode");
+    *dst = std::move(out);
+    return Status::Ok();
+}
+
+Status FEC::DecodeBatchShared(const std::vector<std::vector<std::shared_ptr<const Share>>>& msgs,
+                              std::vector<std::vector<uint8_t>>* out, std::vector<Status>* st) {
+    const int B = static_cast<int>(msgs.size());
+    out->assign(B, {});
+    st->assign(B, Status::Ok());
+    if (B == 0) return Status::Ok();
+    const size_t S = msgs[0].empty() ? 0 : msgs[0][0]->Data.size();
+    std::vector<int> counts(B), nums;
+    std::vector<const uint8_t*> ptrs;
+    for (int b = 0; b < B; ++b) {
+        counts[b] = static_cast<int>(msgs[b].size());
+        for (const std::shared_ptr<const Share>& s : msgs[b]) {
+            if (s->Data.size() != S) return from(RS_ESHARE_LEN, "DecodeBatch");
+            nums.push_back(s->Number);
+            ptrs.push_back(s->Data.data());
+        }
+    }
+    std::vector<uint8_t*> dsts(B);
+    for (int b = 0; b < B; ++b) {
+        (*out)[b].resize(static_cast<size_t>(k_) * S);
+        dsts[b] = (*out)[b].data();
+    }
+    std::vector<int> codes(B, 0);
+    const int rc = rs_decode_batch(ctx_, B, counts.data(), nums.data(), ptrs.data(), S, dsts.data(),
+                                   codes.data());
+    for (int b = 0; b < B; ++b)
+        if (codes[b] != RS_OK) {
+            (*st)[b] = from(codes[b], "Decode");
+            (*out)[b].clear();
+        }
+    return rc == RS_OK ? Status::Ok() : from(rc, "DecodeBatch");
+}
+
 }  // namespace rsmi_host

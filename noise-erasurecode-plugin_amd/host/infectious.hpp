@@ -63,6 +63,12 @@ public:
     // (rs_decode_batch); (*out)[b] / (*st)[b] per message.
     Status DecodeBatch(std::vector<std::vector<Share>>& msgs, std::vector<std::vector<uint8_t>>* out,
                        std::vector<Status>* st);
+    // The same over shares held by shared ownership (the plugin's mempool
+    // snapshots, ShardPlugin::Receive): nothing is copied in, and the
+    // caller's order is left alone (the pool's order carries no meaning).
+    Status DecodeShared(std::vector<uint8_t>* dst, const std::vector<std::shared_ptr<const Share>>& shares);
+    Status DecodeBatchShared(const std::vector<std::vector<std::shared_ptr<const Share>>>& msgs,
+                             std::vector<std::vector<uint8_t>>* out, std::vector<Status>* st);
 
 private:
     friend Status NewFEC(int k, int n, std::shared_ptr<FEC>* out);

@@ -128,8 +128,16 @@ PYBIND11_MODULE(_rsmi_host, m) {
         .def_readwrite("TotalShards", &ShardPlugin::TotalShards)
         .def("Receive",
              [](ShardPlugin& p, const PeerID& sender, const Shard& msg) {
+                 // noise calls Receive once per peer connection, concurrently
+                 // (main.go:49-52): the GIL is released so Python threads do
+                 // too (the sign/verify callbacks take it back).
                  ReceiveEvent ev;
-                 check(p.Receive(sender, msg, &ev));
+                 Status st;
+                 {
+                     py::gil_scoped_release nogil;
+                     st = p.Receive(sender, msg, &ev);
+                 }
+                 check(st);
                  return ev;
              })
         .def("ReceiveBatch",

@@ -235,33 +235,42 @@ Status ShardPlugin::Receive(const PeerID& sender, const Shard& msg, ReceiveEvent
     ReceiveEvent& e = ev ? *ev : local;
     e = ReceiveEvent{};
     const std::string key = HexString(msg.FileSignature);
-    std::vector<Share> pool;
+    std::vector<PoolEntry> pool;
+    PoolEntry mine;  // this shard as a pool entry, built outside the lock
     {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::unique_lock<std::mutex> lk(mu_);
         auto it = shards_.find(key);
-        if (it == shards_.end()) {  // main.go:56-62
-            shards_[key].push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
-            e.pooled = true;
-            return Status::Ok();
+        const bool pools = it == shards_.end() ||
+                           static_cast<int64_t>(it->second.size()) < static_cast<int64_t>(msg.MinimumNeededShards);
+        if (pools) {
+            // main.go:56-62 / :65-71: the share joins the pool.  Its bytes are
+            // copied with the lock released; the pool is looked up again after
+            // (another Receive may have changed it meanwhile, as the
+            // reference's Load/Delete/Store sequence allows).
+            lk.unlock();
+            mine = std::make_shared<const Share>(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+            lk.lock();
+            it = shards_.find(key);
+            if (it == shards_.end() ||
+                static_cast<int64_t>(it->second.size()) < static_cast<int64_t>(msg.MinimumNeededShards)) {
+                shards_[key].push_back(std::move(mine));
+                e.pooled = true;
+                return Status::Ok();
+            }
         }
-        std::vector<Share>& p = it->second;
+        std::vector<PoolEntry>& p = it->second;
         const int64_t len = static_cast<int64_t>(p.size());
-        if (len < static_cast<int64_t>(msg.MinimumNeededShards)) {  // main.go:65-71
-            p.push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
-            e.pooled = true;
-            return Status::Ok();
-        }
         if (!(len >= static_cast<int64_t>(msg.MinimumNeededShards) &&
               len <= static_cast<int64_t>(msg.TotalShards)))  // main.go:100-101
             return Status::Err(RS_EINVAL, "Shards mempool is larger than maximum size");
-        pool = p;  // decode a snapshot outside the lock
+        pool = p;  // k shared pointers: the decode reads the bytes outside the lock
     }
     // main.go:72-99: k and n come from the message.
     e.decoded = true;
     std::shared_ptr<FEC> f;
     e.decode_status = CachedFEC(static_cast<int>(msg.MinimumNeededShards),
                                 static_cast<int>(msg.TotalShards), &f);
-    if (e.decode_status.ok()) e.decode_status = f->Decode(&e.message, pool);
+    if (e.decode_status.ok()) e.decode_status = f->DecodeShared(&e.message, pool);
     if (!e.decode_status.ok()) e.message.clear();
     if (e.decode_status.ok() && verify_) {
         std::vector<std::vector<uint8_t>> h;
@@ -284,7 +293,7 @@ void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs
     struct Job {
         size_t msg;
         std::string key;
-        std::vector<Share> pool;
+        std::vector<PoolEntry> pool;
     };
     std::vector<size_t> pending(msgs.size());
     for (size_t i = 0; i < msgs.size(); ++i) pending[i] = i;
@@ -304,14 +313,15 @@ void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs
                 }
                 auto it = shards_.find(key);
                 if (it == shards_.end()) {
-                    shards_[key].push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+                    shards_[key].push_back(
+                        std::make_shared<const Share>(Share{static_cast<int>(msg.ShardNumber), msg.ShardData}));
                     e.pooled = true;
                     continue;
                 }
-                std::vector<Share>& p = it->second;
+                std::vector<PoolEntry>& p = it->second;
                 const int64_t len = static_cast<int64_t>(p.size());
                 if (len < static_cast<int64_t>(msg.MinimumNeededShards)) {
-                    p.push_back(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+                    p.push_back(std::make_shared<const Share>(Share{static_cast<int>(msg.ShardNumber), msg.ShardData}));
                     e.pooled = true;
                     continue;
                 }
@@ -342,7 +352,7 @@ void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs
         std::map<std::tuple<uint64_t, uint64_t, size_t>, std::vector<size_t>> groups;
         for (size_t j = 0; j < jobs.size(); ++j) {
             const Shard& m = msgs[jobs[j].msg].second;
-            const size_t S = jobs[j].pool.empty() ? 0 : jobs[j].pool[0].Data.size();
+            const size_t S = jobs[j].pool.empty() ? 0 : jobs[j].pool[0]->Data.size();
             groups[{m.MinimumNeededShards, m.TotalShards, S}].push_back(j);
         }
         for (auto& g : groups) {
@@ -351,19 +361,19 @@ void ShardPlugin::ReceiveBatch(const std::vector<std::pair<PeerID, Shard>>& msgs
             std::shared_ptr<FEC> f;
             Status fs = CachedFEC(static_cast<int>(std::get<0>(g.first)),
                                   static_cast<int>(std::get<1>(g.first)), &f);
-            std::vector<std::vector<Share>> pools;
+            std::vector<std::vector<PoolEntry>> pools;
             std::vector<std::vector<uint8_t>> outs;
             std::vector<Status> st;
             bool uniform = true;  // a pool with mixed share lengths goes alone
             for (size_t j : ids)
-                for (const Share& s : jobs[j].pool) uniform &= s.Data.size() == std::get<2>(g.first);
+                for (const PoolEntry& s : jobs[j].pool) uniform &= s->Data.size() == std::get<2>(g.first);
             if (fs.ok() && uniform) {
                 for (size_t j : ids) pools.push_back(jobs[j].pool);
-                f->DecodeBatch(pools, &outs, &st);
+                f->DecodeBatchShared(pools, &outs, &st);
             } else {
                 for (size_t j : ids) {
                     std::vector<uint8_t> o;
-                    Status s1 = fs.ok() ? f->Decode(&o, jobs[j].pool) : fs;
+                    Status s1 = fs.ok() ? f->DecodeShared(&o, jobs[j].pool) : fs;
                     outs.push_back(std::move(o));
                     st.push_back(s1);
                 }

@@ -130,7 +130,12 @@ private:
     Signer sign_;
     Verifier verify_;
     mutable std::mutex mu_;
-    std::unordered_map<std::string, std::vector<Share>> shards_;  // key: hex(signature)
+    // key: hex(signature).  Shares are held by shared ownership: a decode
+    // snapshots the pool (k pointer copies) under mu_ and reads the bytes
+    // after releasing it, like the Go slice the reference stores
+    // (main.go:72-77 decodes the pool's own backing array).
+    using PoolEntry = std::shared_ptr<const Share>;
+    std::unordered_map<std::string, std::vector<PoolEntry>> shards_;
 };
 
 // NewShardPlugin(signaturePolicy, hashPolicy, k, n)  main.go:108-115;

@@ -397,3 +397,59 @@ def test_prepare_shards_hash_overlaps_encode():
     S = len(blob) // k
     assert b"".join(s.ShardData for s in shards[k:]) == par
     assert min(ts) < 0.008, ts  # host hash ~1.2-1.7 ms + encode 0.13 ms; the GPU chain alone is ~15 ms
+
+
+def test_concurrent_receive_config1_blobs():
+    """8 threads call Receive at once (noise runs it once per peer
+    connection, main.go:49-52) on the shards of 8 config-1-sized messages,
+    deliveries shuffled across threads: every message is pooled to k and
+    decoded exactly once, by its k+1-th shard, bit-exact against the oracle's
+    encoding of the same blob; the pool is snapshotted by shared pointers, so
+    decodes read shares while other threads pool into the same map."""
+    import threading
+    k, n = 10, 14
+    E = oracle.fec_matrix(k, n)
+    p = plugin(k, n)
+    blobs, wires, sigs = [], [], []
+    rng = np.random.default_rng(0xC0C0)
+    for b in range(8):
+        blob = oracle.splitmix_bytes(1 << 20, 0x5EED + b).tobytes() + b"\0" * 4
+        shards = p.prepareShards(SELF, blob)
+        assert b"".join(s.ShardData for s in shards[k:]) == oracle.encode(E, k, n, blob)
+        blobs.append(blob)
+        sigs.append(shards[0].FileSignature)
+        lost = set(rng.choice(n, size=n - k - 1, replace=False).tolist())  # k + 1 arrive
+        wires.append([shards[i].Marshal() for i in range(n) if i not in lost])
+    deliveries = [(b, w) for b in range(8) for w in wires[b]]
+    order = rng.permutation(len(deliveries))
+    per_thread = [[deliveries[j] for j in order[t::8]] for t in range(8)]
+    recv = plugin(k, n)
+    events, errors = [], []
+    lock = threading.Lock()
+    start = threading.Barrier(8)
+
+    def run(items):
+        try:
+            start.wait()
+            for b, w in items:
+                s = h.Shard()
+                s.Unmarshal(w)
+                ev = recv.Receive(SELF, s)
+                with lock:
+                    events.append((b, ev.pooled, ev.decoded, ev.verified, ev.message if ev.decoded else None))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=run, args=(items,)) for items in per_thread]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert len(events) == len(deliveries)
+    for b in range(8):
+        mine = [e for e in events if e[0] == b]
+        assert sum(e[1] for e in mine) == k  # k pooled
+        dec = [e for e in mine if e[2]]
+        assert len(dec) == 1 and dec[0][3] and dec[0][4] == blobs[b], b
+        assert recv.PoolSize(sigs[b]) == 0  # verified: the pool was deleted (main.go:90-92)

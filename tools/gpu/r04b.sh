@@ -25,6 +25,12 @@ for rep in 1 2; do
 done
 cat $O/ab.log
 unset RSMI_LIB
+# config-1 latency: direct-staging host pipeline (default) vs the copy-engine path
+L="--stripes 64 --shard 65536 --steps 2 --warmup 1 --cpu-seconds 0 --config1-reps 200 --config5-stripes 64 --config5-steps 1 --config5-warmup 1"
+for rep in 1 2; do
+  timeout -k 10 200 python3 bench.py $L > $O/c1_direct_$rep.json 2>> $O/c1.err || exit 6
+  RSMI_HOSTPIPE=dma timeout -k 10 200 python3 bench.py $L > $O/c1_dma_$rep.json 2>> $O/c1.err || exit 7
+done
 B="python3 bench.py --steps 2 --warmup 1 $C5"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_WAIT_ANY SQ_INSTS_SALU SQ_WAVES --kernel-trace -d $O/pmc_sq/sq -o run --output-format csv -- $B > $O/sq.log 2>&1 || exit 5
 echo done
