@@ -75,6 +75,22 @@ bool kTopGuard = false;
 // the pattern's id rows (ballots, the pre-r03 prologue), prints any
 // disagreement with the host's mask record and codes with the derived ones.
 bool kDebugMasks = false;
+// Absent inputs' loads (-A): read a present shard at the lane's own offsets
+// (the lines its own load brings in) instead of the 2 KiB zero page at
+// separate offsets -- the loads then differ only in their scalar base, with
+// no per-load offset selects.
+bool kAliasAbsent = false;
+// Reconstruct loads as buffer loads (-B): every input gets a buffer resource
+// (base in SGPRs, 32-bit lane offsets, no address VALU); an absent input's
+// resource has num_records 0, so its loads return zeros without touching
+// memory (no zero page, no per-load offset selects).
+bool kBufferLoads = false;
+// Present inputs are transposed in a local copy of their load registers
+// (-W), so the load ring carries no value across the input's branch.
+bool kWorkCopy = false;
+// Solve tail (-L): a last group of 1-2 outputs runs a 2-output pass instead
+// of a padded R-output one.
+bool kSolveTail = false;
 constexpr int kTopMinM = 12;
 
 void emit_common(FILE* f) {
@@ -152,6 +168,19 @@ __device__ __forceinline__ void bs_combos(const uint32_t* p, uint32_t (&c)[16]) 
 __device__ __forceinline__ void bs_load(uint32_t (&x)[8], const uint8_t* shard, uint32_t offa, uint32_t offb) {
     const bs_u32x4 u = __builtin_nontemporal_load((BsGlobalCU4*)(shard + offa));
     const bs_u32x4 v = __builtin_nontemporal_load((BsGlobalCU4*)(shard + offb));
+    x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w;
+    x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
+}
+
+// Buffer-resource form (gen_bitslice -B): base and range in SGPRs, the lane
+// offset in one VGPR; num_records 0 makes every load return zeros.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bs_rsrc(const uint8_t* base, bool present) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), static_cast<short>(0),
+                                             present ? 0x7FFFFFFF : 0, 0x00020000);
+}
+__device__ __forceinline__ void bs_load_buf(uint32_t (&x)[8], __amdgpu_buffer_rsrc_t r, uint32_t offa, uint32_t offb) {
+    const bs_u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, offa, 0, 2);  // 2: nt
+    const bs_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, offb, 0, 2);
     x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w;
     x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
 }
@@ -429,11 +458,23 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
     // every block, so they stay in L2: no HBM traffic) and its network step
     // is skipped.  Loads under a branch made the compiler wait for every load
     // in flight (vmcnt(0)) at each input, i.e. no prefetch at all.
-    std::fprintf(f, "    const uint32_t zoffa = lane * 16u, zoffb = 1024u + lane * 16u;\n");
+    if (kBufferLoads)
+        ;  // no zero page: absent inputs get an empty buffer range
+    else if (kAliasAbsent)
+        std::fprintf(f, "    // absent inputs alias the first present shard (data, else a parity survivor)\n"
+                        "    const uint8_t* alias = dmask ? shard(static_cast<uint32_t>(__builtin_ctzll(dmask)))\n"
+                        "                                 : shard(static_cast<uint32_t>(K + __builtin_ctz(pmask)));\n");
+    else
+        std::fprintf(f, "    const uint32_t zoffa = lane * 16u, zoffb = 1024u + lane * 16u;\n");
     auto emit_load = [&](int j, int buf) {
         const std::string pr = pres(j);
-        std::fprintf(f, "    bs_load(x[%d], %s ? %s : a.zpage, %s ? offa : zoffa, %s ? offb : zoffb);\n", buf,
-                     pr.c_str(), ptr(j).c_str(), pr.c_str(), pr.c_str());
+        if (kBufferLoads)
+            std::fprintf(f, "    bs_load_buf(x[%d], bs_rsrc(%s, %s), offa, offb);\n", buf, ptr(j).c_str(), pr.c_str());
+        else if (kAliasAbsent)
+            std::fprintf(f, "    bs_load(x[%d], %s ? %s : alias, offa, offb);\n", buf, pr.c_str(), ptr(j).c_str());
+        else
+            std::fprintf(f, "    bs_load(x[%d], %s ? %s : a.zpage, %s ? offa : zoffa, %s ? offb : zoffb);\n", buf,
+                         pr.c_str(), ptr(j).c_str(), pr.c_str(), pr.c_str());
     };
     for (int j = 0; j < PF && j < N; ++j) emit_load(j, j);
     std::fprintf(f, "%s", R"(    // slot_t[t]: the erased data slot parity survivor t fills.  Rebuild walks
@@ -478,20 +519,26 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
         if (j + PF < N)
             emit_load(j + PF, (j + PF) % (PF + 1));
         std::fprintf(f, "    if (%s) {\n", pres(j).c_str());
-        std::fprintf(f, "        asm volatile(\"\" : \"+v\"(x[%d][0]), \"+v\"(x[%d][1]), \"+v\"(x[%d][2]), \"+v\"(x[%d][3]), "
-                        "\"+v\"(x[%d][4]), \"+v\"(x[%d][5]), \"+v\"(x[%d][6]), \"+v\"(x[%d][7]));\n",
-                     buf, buf, buf, buf, buf, buf, buf, buf);
+        std::string xb = "x[" + std::to_string(buf) + "]";
+        if (kWorkCopy) {
+            std::fprintf(f, "        uint32_t xw[8] = {x[%d][0], x[%d][1], x[%d][2], x[%d][3], x[%d][4], x[%d][5], x[%d][6], x[%d][7]};\n",
+                         buf, buf, buf, buf, buf, buf, buf, buf);
+            xb = "xw";
+        }
+        std::fprintf(f, "        asm volatile(\"\" : \"+v\"(%s[0]), \"+v\"(%s[1]), \"+v\"(%s[2]), \"+v\"(%s[3]), "
+                        "\"+v\"(%s[4]), \"+v\"(%s[5]), \"+v\"(%s[6]), \"+v\"(%s[7]));\n",
+                     xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str());
         if (kMovementOnly) {
             // movement twin: the input only enters one row's accumulators
             const int t = (j % top) * 8;
-            for (int q = 0; q < 8; ++q) std::fprintf(f, "        acc[%d] ^= x[%d][%d];\n", t + q, buf, q);
+            for (int q = 0; q < 8; ++q) std::fprintf(f, "        acc[%d] ^= %s[%d];\n", t + q, xb.c_str(), q);
             std::fprintf(f, "    }\n");
             continue;
         }
         if (j < k) {
-            std::fprintf(f, "        bs_to_planes(x[%d]);\n", buf);
-            std::fprintf(f, "        uint32_t c1[16], c2[16];\n        bs_combos(&x[%d][0], c1);\n"
-                            "        bs_combos(&x[%d][4], c2);\n", buf, buf);
+            std::fprintf(f, "        bs_to_planes(%s);\n", xb.c_str());
+            std::fprintf(f, "        uint32_t c1[16], c2[16];\n        bs_combos(&%s[0], c1);\n"
+                            "        bs_combos(&%s[4], c2);\n", xb.c_str(), xb.c_str());
             emit_network(f, E, k, m, j, false, top < m && !kTopGuard ? nullptr : "rmask", T0);
             emit_acc_fence(f, 0, P);
         } else {
@@ -503,7 +550,7 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
             std::fprintf(f, "        uint32_t w[8] = {acc[%d], acc[%d], acc[%d], acc[%d], acc[%d], acc[%d], acc[%d], acc[%d]};\n"
                             "        bs_from_planes(w);\n",
                          t * 8, t * 8 + 1, t * 8 + 2, t * 8 + 3, t * 8 + 4, t * 8 + 5, t * 8 + 6, t * 8 + 7);
-            for (int q = 0; q < 8; ++q) std::fprintf(f, "        acc[%d] = w[%d] ^ x[%d][%d];\n", t * 8 + q, q, buf, q);
+            for (int q = 0; q < 8; ++q) std::fprintf(f, "        acc[%d] = w[%d] ^ %s[%d];\n", t * 8 + q, q, xb.c_str(), q);
             emit_acc_fence(f, t * 8, t * 8 + 8);
         }
         std::fprintf(f, "    }\n");
@@ -548,15 +595,14 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[8 * (t - T0) + i] = w[i];
         }
-#pragma unroll 1
-    for (uint32_t g = 0; g < e; g += R) {
-        uint32_t oid[R];
+)");
+    const char* solve_body = R"SOLVE(        uint32_t oid[RR];
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+        for (int r = 0; r < RR; ++r)
             oid[r] = g + r < e ? static_cast<uint32_t>(__builtin_amdgcn_readlane(did_l, g + r)) : 0xFFFFFFFFu;
-        uint32_t out[R][8];
+        uint32_t out[RR][8];
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+        for (int r = 0; r < RR; ++r)
 #pragma unroll
             for (int w = 0; w < 8; ++w) out[r][w] = 0u;
 #pragma unroll
@@ -567,39 +613,44 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
                 // hoists every syndrome's bit fields: ~100 extra VGPRs).
                 asm volatile("" : "+v"(acc[at + 0]), "+v"(acc[at + 1]), "+v"(acc[at + 2]), "+v"(acc[at + 3]),
                                   "+v"(acc[at + 4]), "+v"(acc[at + 5]), "+v"(acc[at + 6]), "+v"(acc[at + 7]));
-                uint32_t T[R][5];
+                uint32_t T[RR][5];
 #pragma unroll
-                for (int r = 0; r < R; ++r)
+                for (int r = 0; r < RR; ++r)
 #pragma unroll
                     for (int i = 0; i < 5; ++i) T[r][i] = mtab[g + r][t - T0][i];
 #pragma unroll
                 for (int w = 0; w < 8; ++w) {
                     const gfd::Fields fl = gfd::fields(acc[at + w]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) out[r][w] = gfd::gf_mac(out[r][w], T[r], fl.a, fl.b, fl.c);
+                    for (int r = 0; r < RR; ++r) out[r][w] = gfd::gf_mac(out[r][w], T[r], fl.a, fl.b, fl.c);
                 }
             }
             if ((qmask >> t) & 1u) {
 #pragma unroll
-                for (int r = 0; r < R; ++r)
+                for (int r = 0; r < RR; ++r)
                     if (oid[r] == static_cast<uint32_t>(K + t)) {
 #pragma unroll
                         for (int w = 0; w < 8; ++w) out[r][w] ^= acc[at + w];
                     }
             }
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+            for (int r = 0; r < RR; ++r)
                 asm volatile("" : "+v"(out[r][0]), "+v"(out[r][1]), "+v"(out[r][2]), "+v"(out[r][3]),
                                   "+v"(out[r][4]), "+v"(out[r][5]), "+v"(out[r][6]), "+v"(out[r][7])::"memory");
         }
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+        for (int r = 0; r < RR; ++r) {
             if (g + r >= e) break;
             uint8_t* o = shard(oid[r]);
             if (oka) bs_store(o, offa, out[r][0], out[r][1], out[r][2], out[r][3]);
             if (okb) bs_store(o, offb, out[r][4], out[r][5], out[r][6], out[r][7]);
         }
-    }
+)SOLVE";
+    std::fprintf(f, "#pragma unroll 1\n    for (uint32_t g = 0; g < e; g += R) {\n");
+    if (kSolveTail)
+        std::fprintf(f, "    if (e - g <= 2u) {\n    constexpr int RR = 2;\n%s    break;\n    }\n", solve_body);
+    std::fprintf(f, "    {\n    constexpr int RR = R;\n%s    }\n", solve_body);
+    std::fprintf(f, "%s", R"(    }
     }  // column window
 }
 
@@ -682,6 +733,26 @@ int main(int argc, char** argv) {
         argv += 1;
         argc -= 1;
     }
+    if (argc >= 2 && std::string(argv[1]) == "-A") {
+        kAliasAbsent = true;
+        argv += 1;
+        argc -= 1;
+    }
+    if (argc >= 2 && std::string(argv[1]) == "-B") {
+        kBufferLoads = true;
+        argv += 1;
+        argc -= 1;
+    }
+    if (argc >= 2 && std::string(argv[1]) == "-W") {
+        kWorkCopy = true;
+        argv += 1;
+        argc -= 1;
+    }
+    if (argc >= 2 && std::string(argv[1]) == "-L") {
+        kSolveTail = true;
+        argv += 1;
+        argc -= 1;
+    }
     if (argc >= 2 && std::string(argv[1]) == "-u") {
         kTopGuard = true;
         argv += 1;
@@ -721,7 +792,7 @@ int main(int argc, char** argv) {
         argc -= 2;
     }
     if (argc < 3) {
-        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-E] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-A] [-B] [-W] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
         return 2;
     }
     std::vector<std::pair<int, int>> codes;

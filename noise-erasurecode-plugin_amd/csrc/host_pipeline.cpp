@@ -2,6 +2,7 @@
 #include "host_pipeline.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -22,6 +23,8 @@ int pool_threads() {
 
 // ------------------------------------------------------------ CopyPool ----
 CopyPool::CopyPool(int threads) {
+    const char* e = std::getenv("RSMI_COPY_SPIN_US");
+    spin_us_ = e ? std::max(0, std::min(std::atoi(e), 10000)) : 0;
     for (int i = 0; i < threads - 1; ++i) threads_.emplace_back([this] { worker(); });
 }
 
@@ -54,12 +57,21 @@ void CopyPool::copy_part(const Job& j, size_t part) {
 void CopyPool::worker() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
+        if (jobs_.empty() && spin_us_ > 0 && !stop_) {
+            // Out of work: spin a while for the next job before sleeping.
+            lk.unlock();
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+            while (queued_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+                __builtin_ia32_pause();
+            lk.lock();
+        }
         cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
         if (stop_) return;
         Job* j = jobs_.front();
         size_t part = 0;
         if (!claim(j, &part)) {  // every part handed out: the job leaves the queue
             jobs_.pop_front();
+            queued_.fetch_sub(1, std::memory_order_release);
             continue;
         }
         lk.unlock();
@@ -92,6 +104,7 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
     }
     std::unique_lock<std::mutex> lk(mu_);
     jobs_.push_back(&job);
+    queued_.fetch_add(1, std::memory_order_release);
     cv_.notify_all();
     // The calling thread works on its own job.  Workers only touch `job`
     // under mu_ while it is queued or after claiming a part (finished <
@@ -107,6 +120,7 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
     for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
         if (*it == &job) {
             jobs_.erase(it);
+            queued_.fetch_sub(1, std::memory_order_release);
             break;
         }
 }
@@ -188,8 +202,11 @@ hipError_t HostPipeline::drain(Slot& s, uint8_t* const* dsts, int e) {
 }
 
 hipError_t HostPipeline::run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e,
-                             size_t S, const ChunkLaunch& launch) {
-    if (S == 0 || e == 0) return hipSuccess;
+                             size_t S, const ChunkLaunch& launch, const std::function<void()>& while_gpu) {
+    if (S == 0 || e == 0) {
+        if (while_gpu) while_gpu();
+        return hipSuccess;
+    }
     // Column chunk per shard: about kChunkBytes of survivors per chunk
     // (RSMI_HOSTPIPE_CHUNK overrides, for A/B runs).
     static const size_t chunk_bytes = [] {
@@ -229,6 +246,7 @@ hipError_t HostPipeline::run(const uint8_t* const* srcs, int k, uint8_t* const* 
             s.pitch = cb;
         }
     }
+    if (while_gpu) while_gpu();
     // Drain the last chunks in order (also after an error, so no slot is
     // left holding a pending copy into caller memory).
     for (size_t i = 0; i < kSlots; ++i) {

@@ -15,6 +15,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
@@ -40,6 +41,10 @@ public:
     };
     // Copies every piece (split further into <= 1 MiB parts); returns when done.
     void run(const std::vector<Piece>& pieces);
+    // Workers that run out of parts spin this long for the next job before
+    // sleeping on the condition variable (RSMI_COPY_SPIN_US, default 0): a
+    // burst of small messages then finds them awake.
+    int spin_us() const { return spin_us_; }
     // The process-wide pool (RSMI_COPY_THREADS workers, default min(8, cpus)).
     static CopyPool& shared();
 
@@ -62,6 +67,8 @@ private:
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<Job*> jobs_;
+    std::atomic<int> queued_{0};  // jobs in jobs_ (read without mu_ while spinning)
+    int spin_us_ = 0;
     bool stop_ = false;
 };
 
@@ -75,8 +82,11 @@ public:
     HostPipeline();
     ~HostPipeline();
     // out_t[0..S) = f(srcs[0..k)[0..S)) for t < e, streamed in chunks.
+    // while_gpu (optional) runs on the calling thread once every chunk is
+    // queued and before the last ones are drained: host work that overlaps
+    // the GPU's (rs_decode copies the present data shares into dst there).
     hipError_t run(const uint8_t* const* srcs, int k, uint8_t* const* dsts, int e, size_t S,
-                   const ChunkLaunch& launch);
+                   const ChunkLaunch& launch, const std::function<void()>& while_gpu = nullptr);
 
     // Parallel pageable <-> pinned copies on the shared worker pool.
     void copy(const std::vector<CopyPool::Piece>& pieces) { pool_.run(pieces); }

@@ -10,6 +10,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <functional>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -206,6 +207,7 @@ struct Lease {
     hipEvent_t ev[kBatchChunks] = {};  // rs_decode_batch D2H chunk events
     Staging st_stripe;                 // stripe descriptors
     Staging st_batch, st_pieces;       // rs_decode_batch
+    Staging st_onepat;                 // host-API decode: the one-pattern table, read in place by the kernel
     DevBuf d_stripe_pat, d_batch, d_pack, d_pieces, d_onepat;
     std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
     std::vector<uint32_t> pid, start;          // reconstruct scratch
@@ -245,6 +247,7 @@ struct Lease {
         st_stripe.destroy();
         st_batch.destroy();
         st_pieces.destroy();
+        st_onepat.destroy();
         for (DevBuf* b : {&d_stripe_pat, &d_batch, &d_pack, &d_pieces, &d_onepat}) b->release();
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -917,9 +920,13 @@ int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_
 // out_t = decode row (surv -> targets[t]) applied to the survivors, on the
 // GPU through L's pinned host pipeline.  Runs on c->device.
 int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vector<const uint8_t*>& surv_ptr,
-             const std::vector<int>& targets, const std::vector<uint8_t*>& outs, size_t S) {
+             const std::vector<int>& targets, const std::vector<uint8_t*>& outs, size_t S,
+             const std::function<void()>& while_gpu = nullptr) {
     const int k = c->k, e = static_cast<int>(targets.size());
-    if (e == 0 || S == 0) return RS_OK;
+    if (e == 0 || S == 0) {
+        if (while_gpu) while_gpu();
+        return RS_OK;
+    }
     std::vector<uint8_t> rows;
     if (!rsmi::decode_rows(c->enc, k, c->n, surv, targets, rows)) return RS_ESINGULAR;
     rsmi::HostPipeline* pipe = L.pipeline();
@@ -934,21 +941,36 @@ int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vecto
         std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(et));
         for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
         for (int t = 0; t < et; ++t) dstid[t] = static_cast<uint32_t>(k + t);
-        std::vector<uint8_t> hp(PatLayout(c, 1).total);
-        pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
-        // The previous pass's launches were drained by pipe->run.
-        if (!L.d_onepat.reserve_on(hp.size(), L.stream)) return RS_ENOMEM;
-        if (hipMemcpyAsync(L.d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice, L.stream) != hipSuccess ||
-            hipStreamSynchronize(L.stream) != hipSuccess)
-            return RS_EDEVICE;
-        const void* pat = L.d_onepat.p;
+        const size_t pbytes = PatLayout(c, 1).total;
+        const void* pat = nullptr;
+        if (pipe->direct()) {
+            // The kernel reads the one-pattern table straight from pinned
+            // host memory (its device alias), like the survivors: no upload
+            // and no stream sync before the launch.  The previous pass's
+            // launches were drained by pipe->run.
+            if (!L.st_onepat.acquire(pbytes)) return RS_ENOMEM;
+            pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(),
+                          static_cast<uint8_t*>(L.st_onepat.p));
+            void* alias = nullptr;
+            if (hipHostGetDevicePointer(&alias, L.st_onepat.p, 0) != hipSuccess) alias = L.st_onepat.p;
+            pat = alias;
+        } else {
+            std::vector<uint8_t> hp(pbytes);
+            pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
+            if (!L.d_onepat.reserve_on(hp.size(), L.stream)) return RS_ENOMEM;
+            if (hipMemcpyAsync(L.d_onepat.p, hp.data(), hp.size(), hipMemcpyHostToDevice, L.stream) != hipSuccess ||
+                hipStreamSynchronize(L.stream) != hipSuccess)
+                return RS_EDEVICE;
+            pat = L.d_onepat.p;
+        }
         auto launch = [c, et, pat](uint8_t* din, uint8_t* dout, size_t pitch, size_t w, hipStream_t st) {
             rsmi::MatArgs a = base_args(c, din, 0, dout, 0, pitch, w, 1);
             set_patterns(c, 1, pat, a);
             a.stripe_desc = first_stripe_desc(c, pat);  // et outputs, not m
             return rsmi::launch_matmul(a, et, st);
         };
-        const hipError_t err = pipe->run(surv_ptr.data(), k, outs.data() + t0, et, S, launch);
+        const hipError_t err = pipe->run(surv_ptr.data(), k, outs.data() + t0, et, S, launch,
+                                         t0 == 0 ? while_gpu : std::function<void()>());
         if (err != hipSuccess) return RS_EDEVICE;
     }
     return RS_OK;
@@ -1004,11 +1026,15 @@ int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
             missing.push_back(i);
             outs.push_back(dst + static_cast<size_t>(i) * S);
         }
-    const int st = gpu_rows(c, L, surv, sp, missing, outs, S);
-    if (st != RS_OK) return st;
-    for (int i = 0; i < k; ++i)
-        if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
-    return RS_OK;
+    // The present data shares go to dst on the copy pool while the GPU
+    // regenerates the missing ones (gpu_rows' overlap hook).
+    auto copy_present = [&] {
+        std::vector<rsmi::CopyPool::Piece> pieces;
+        for (int i = 0; i < k; ++i)
+            if (present[i]) pieces.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
+        rsmi::CopyPool::shared().run(pieces);
+    };
+    return gpu_rows(c, L, surv, sp, missing, outs, S, copy_present);
 }
 
 // Columns where any of `outs` differs from the received shares `recv`.
