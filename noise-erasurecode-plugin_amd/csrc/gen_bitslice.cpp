@@ -75,21 +75,16 @@ bool kTopGuard = false;
 // the pattern's id rows (ballots, the pre-r03 prologue), prints any
 // disagreement with the host's mask record and codes with the derived ones.
 bool kDebugMasks = false;
-// Absent inputs' loads (-A): read a present shard at the lane's own offsets
-// (the lines its own load brings in) instead of the 2 KiB zero page at
-// separate offsets -- the loads then differ only in their scalar base, with
-// no per-load offset selects.
-bool kAliasAbsent = false;
-// Reconstruct loads as buffer loads (-B): every input gets a buffer resource
-// (base in SGPRs, 32-bit lane offsets, no address VALU); an absent input's
-// resource has num_records 0, so its loads return zeros without touching
-// memory (no zero page, no per-load offset selects).
-bool kBufferLoads = false;
-// Present inputs are transposed in a local copy of their load registers
-// (-W), so the load ring carries no value across the input's branch.
-bool kWorkCopy = false;
-// Solve tail (-L): a last group of 1-2 outputs runs a 2-output pass instead
-// of a padded R-output one.
+// Reconstruct loads as buffer loads (default; -Z restores the round-3 zero
+// page): every input gets a buffer resource (base in SGPRs, 32-bit lane
+// offsets, no address VALU); an absent input's resource has num_records 0, so
+// its loads return zeros without touching memory (no zero page, no per-load
+// offset selects).  Same-box A/B, 10 steps x 2 (profiles/r04c/): config 5
+// reconstruct fresh 1-16 -1.7%, 16 erasures -1.1%, RS(8,14) -2.5%.
+bool kBufferLoads = true;
+// Solve tail (-L): outputs past e in the last group of R are skipped by a
+// wave-uniform branch per (syndrome, output) instead of coded as padding;
+// the syndrome's bit fields are extracted once per group for all outputs.
 bool kSolveTail = false;
 constexpr int kTopMinM = 12;
 
@@ -458,20 +453,12 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
     // every block, so they stay in L2: no HBM traffic) and its network step
     // is skipped.  Loads under a branch made the compiler wait for every load
     // in flight (vmcnt(0)) at each input, i.e. no prefetch at all.
-    if (kBufferLoads)
-        ;  // no zero page: absent inputs get an empty buffer range
-    else if (kAliasAbsent)
-        std::fprintf(f, "    // absent inputs alias the first present shard (data, else a parity survivor)\n"
-                        "    const uint8_t* alias = dmask ? shard(static_cast<uint32_t>(__builtin_ctzll(dmask)))\n"
-                        "                                 : shard(static_cast<uint32_t>(K + __builtin_ctz(pmask)));\n");
-    else
+    if (!kBufferLoads)  // (buffer loads: absent inputs get an empty range, no zero page)
         std::fprintf(f, "    const uint32_t zoffa = lane * 16u, zoffb = 1024u + lane * 16u;\n");
     auto emit_load = [&](int j, int buf) {
         const std::string pr = pres(j);
         if (kBufferLoads)
             std::fprintf(f, "    bs_load_buf(x[%d], bs_rsrc(%s, %s), offa, offb);\n", buf, ptr(j).c_str(), pr.c_str());
-        else if (kAliasAbsent)
-            std::fprintf(f, "    bs_load(x[%d], %s ? %s : alias, offa, offb);\n", buf, pr.c_str(), ptr(j).c_str());
         else
             std::fprintf(f, "    bs_load(x[%d], %s ? %s : a.zpage, %s ? offa : zoffa, %s ? offb : zoffb);\n", buf,
                          pr.c_str(), ptr(j).c_str(), pr.c_str(), pr.c_str());
@@ -519,12 +506,7 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
         if (j + PF < N)
             emit_load(j + PF, (j + PF) % (PF + 1));
         std::fprintf(f, "    if (%s) {\n", pres(j).c_str());
-        std::string xb = "x[" + std::to_string(buf) + "]";
-        if (kWorkCopy) {
-            std::fprintf(f, "        uint32_t xw[8] = {x[%d][0], x[%d][1], x[%d][2], x[%d][3], x[%d][4], x[%d][5], x[%d][6], x[%d][7]};\n",
-                         buf, buf, buf, buf, buf, buf, buf, buf);
-            xb = "xw";
-        }
+        const std::string xb = "x[" + std::to_string(buf) + "]";
         std::fprintf(f, "        asm volatile(\"\" : \"+v\"(%s[0]), \"+v\"(%s[1]), \"+v\"(%s[2]), \"+v\"(%s[3]), "
                         "\"+v\"(%s[4]), \"+v\"(%s[5]), \"+v\"(%s[6]), \"+v\"(%s[7]));\n",
                      xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str());
@@ -596,13 +578,14 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
             for (int i = 0; i < 8; ++i) acc[8 * (t - T0) + i] = w[i];
         }
 )");
-    const char* solve_body = R"SOLVE(        uint32_t oid[RR];
+    std::fprintf(f, "#pragma unroll 1\n    for (uint32_t g = 0; g < e; g += R) {\n%s",
+                 kSolveTail ? R"SOLVE(        uint32_t oid[R];
 #pragma unroll
-        for (int r = 0; r < RR; ++r)
+        for (int r = 0; r < R; ++r)
             oid[r] = g + r < e ? static_cast<uint32_t>(__builtin_amdgcn_readlane(did_l, g + r)) : 0xFFFFFFFFu;
-        uint32_t out[RR][8];
+        uint32_t out[R][8];
 #pragma unroll
-        for (int r = 0; r < RR; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int w = 0; w < 8; ++w) out[r][w] = 0u;
 #pragma unroll
@@ -613,43 +596,95 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
                 // hoists every syndrome's bit fields: ~100 extra VGPRs).
                 asm volatile("" : "+v"(acc[at + 0]), "+v"(acc[at + 1]), "+v"(acc[at + 2]), "+v"(acc[at + 3]),
                                   "+v"(acc[at + 4]), "+v"(acc[at + 5]), "+v"(acc[at + 6]), "+v"(acc[at + 7]));
-                uint32_t T[RR][5];
+                uint32_t T[R][5];
 #pragma unroll
-                for (int r = 0; r < RR; ++r)
+                for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int i = 0; i < 5; ++i) T[r][i] = mtab[g + r][t - T0][i];
+                // Fields of the syndrome's 8 words once; each output of the
+                // group is coded only if it exists (no padded outputs when
+                // e is not a multiple of R).
+                gfd::Fields fl[8];
 #pragma unroll
-                for (int w = 0; w < 8; ++w) {
-                    const gfd::Fields fl = gfd::fields(acc[at + w]);
+                for (int w = 0; w < 8; ++w) fl[w] = gfd::fields(acc[at + w]);
 #pragma unroll
-                    for (int r = 0; r < RR; ++r) out[r][w] = gfd::gf_mac(out[r][w], T[r], fl.a, fl.b, fl.c);
-                }
+                for (int r = 0; r < R; ++r)
+                    if (r == 0 || g + r < e) {
+#pragma unroll
+                        for (int w = 0; w < 8; ++w) out[r][w] = gfd::gf_mac(out[r][w], T[r], fl[w].a, fl[w].b, fl[w].c);
+                    }
             }
             if ((qmask >> t) & 1u) {
 #pragma unroll
-                for (int r = 0; r < RR; ++r)
+                for (int r = 0; r < R; ++r)
                     if (oid[r] == static_cast<uint32_t>(K + t)) {
 #pragma unroll
                         for (int w = 0; w < 8; ++w) out[r][w] ^= acc[at + w];
                     }
             }
 #pragma unroll
-            for (int r = 0; r < RR; ++r)
+            for (int r = 0; r < R; ++r)
                 asm volatile("" : "+v"(out[r][0]), "+v"(out[r][1]), "+v"(out[r][2]), "+v"(out[r][3]),
                                   "+v"(out[r][4]), "+v"(out[r][5]), "+v"(out[r][6]), "+v"(out[r][7])::"memory");
         }
 #pragma unroll
-        for (int r = 0; r < RR; ++r) {
+        for (int r = 0; r < R; ++r) {
             if (g + r >= e) break;
             uint8_t* o = shard(oid[r]);
             if (oka) bs_store(o, offa, out[r][0], out[r][1], out[r][2], out[r][3]);
             if (okb) bs_store(o, offb, out[r][4], out[r][5], out[r][6], out[r][7]);
         }
-)SOLVE";
-    std::fprintf(f, "#pragma unroll 1\n    for (uint32_t g = 0; g < e; g += R) {\n");
-    if (kSolveTail)
-        std::fprintf(f, "    if (e - g <= 2u) {\n    constexpr int RR = 2;\n%s    break;\n    }\n", solve_body);
-    std::fprintf(f, "    {\n    constexpr int RR = R;\n%s    }\n", solve_body);
+)SOLVE"
+                            : R"SOLVE(        uint32_t oid[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            oid[r] = g + r < e ? static_cast<uint32_t>(__builtin_amdgcn_readlane(did_l, g + r)) : 0xFFFFFFFFu;
+        uint32_t out[R][8];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int w = 0; w < 8; ++w) out[r][w] = 0u;
+#pragma unroll
+        for (int t = T0; t < M; ++t) {
+            const int at = 8 * (t - T0);  // row t's accumulators
+            if ((pmask >> t) & 1u) {
+                // Syndrome t's words enter here (otherwise the scheduler
+                // hoists every syndrome's bit fields: ~100 extra VGPRs).
+                asm volatile("" : "+v"(acc[at + 0]), "+v"(acc[at + 1]), "+v"(acc[at + 2]), "+v"(acc[at + 3]),
+                                  "+v"(acc[at + 4]), "+v"(acc[at + 5]), "+v"(acc[at + 6]), "+v"(acc[at + 7]));
+                uint32_t T[R][5];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) T[r][i] = mtab[g + r][t - T0][i];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    const gfd::Fields fl = gfd::fields(acc[at + w]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) out[r][w] = gfd::gf_mac(out[r][w], T[r], fl.a, fl.b, fl.c);
+                }
+            }
+            if ((qmask >> t) & 1u) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (oid[r] == static_cast<uint32_t>(K + t)) {
+#pragma unroll
+                        for (int w = 0; w < 8; ++w) out[r][w] ^= acc[at + w];
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                asm volatile("" : "+v"(out[r][0]), "+v"(out[r][1]), "+v"(out[r][2]), "+v"(out[r][3]),
+                                  "+v"(out[r][4]), "+v"(out[r][5]), "+v"(out[r][6]), "+v"(out[r][7])::"memory");
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (g + r >= e) break;
+            uint8_t* o = shard(oid[r]);
+            if (oka) bs_store(o, offa, out[r][0], out[r][1], out[r][2], out[r][3]);
+            if (okb) bs_store(o, offb, out[r][4], out[r][5], out[r][6], out[r][7]);
+        }
+)SOLVE");
     std::fprintf(f, "%s", R"(    }
     }  // column window
 }
@@ -733,18 +768,13 @@ int main(int argc, char** argv) {
         argv += 1;
         argc -= 1;
     }
-    if (argc >= 2 && std::string(argv[1]) == "-A") {
-        kAliasAbsent = true;
-        argv += 1;
-        argc -= 1;
-    }
     if (argc >= 2 && std::string(argv[1]) == "-B") {
         kBufferLoads = true;
         argv += 1;
         argc -= 1;
     }
-    if (argc >= 2 && std::string(argv[1]) == "-W") {
-        kWorkCopy = true;
+    if (argc >= 2 && std::string(argv[1]) == "-Z") {
+        kBufferLoads = false;
         argv += 1;
         argc -= 1;
     }
@@ -792,7 +822,7 @@ int main(int argc, char** argv) {
         argc -= 2;
     }
     if (argc < 3) {
-        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-A] [-B] [-W] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
         return 2;
     }
     std::vector<std::pair<int, int>> codes;
