@@ -21,6 +21,22 @@ int pool_threads() {
 }
 }  // namespace
 
+hipError_t wait_event(hipEvent_t ev) {
+    static const int spin_us = [] {
+        const char* e = std::getenv("RSMI_SYNC_SPIN_US");
+        return e ? std::max(0, std::min(std::atoi(e), 100000)) : 200;
+    }();
+    if (spin_us > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+        do {
+            const hipError_t q = hipEventQuery(ev);
+            if (q != hipErrorNotReady) return q;
+            __builtin_ia32_pause();
+        } while (std::chrono::steady_clock::now() < until);
+    }
+    return hipEventSynchronize(ev);
+}
+
 // ------------------------------------------------------------ CopyPool ----
 CopyPool::CopyPool(int threads) {
     const char* e = std::getenv("RSMI_COPY_SPIN_US");
@@ -193,7 +209,7 @@ bool HostPipeline::ensure(Slot& s, size_t in_bytes, size_t out_bytes) {
 hipError_t HostPipeline::drain(Slot& s, uint8_t* const* dsts, int e) {
     if (!s.pending) return hipSuccess;
     s.pending = false;
-    const hipError_t err = hipEventSynchronize(s.done);
+    const hipError_t err = wait_event(s.done);
     if (err != hipSuccess) return err;
     std::vector<CopyPool::Piece> out;
     for (int t = 0; t < e; ++t) out.push_back({dsts[t] + s.c0, s.h_out + t * s.pitch, s.w});

@@ -72,6 +72,12 @@ private:
     bool stop_ = false;
 };
 
+// Waits for ev on the host: polls it for up to RSMI_SYNC_SPIN_US
+// microseconds (default 200) before blocking in hipEventSynchronize.  A
+// 1 MiB message's kernel finishes within that window, and the blocking wait's
+// wake-up was a fixed ~10 us of the host API's latency.
+hipError_t wait_event(hipEvent_t ev);
+
 // Launches the GF kernel for one chunk: survivors at din + j*pitch (j < k),
 // outputs at dout + t*pitch, w coded bytes per shard.
 using ChunkLaunch = std::function<hipError_t(uint8_t* din, uint8_t* dout, size_t pitch,

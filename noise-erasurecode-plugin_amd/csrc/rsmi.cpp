@@ -991,21 +991,16 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
     if (!din || !dout) return false;
     const hipStream_t s = L.stream;
     L.begin(s);
-    if (!L.st_pieces.acquire(n * sizeof(uint64_t)) || !L.d_pieces.reserve_on(n * sizeof(uint64_t), s)) {
-        *rc = RS_ENOMEM;
-        return true;
-    }
-    uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
-    for (size_t i = 0; i < n; ++i) tab[i] = i < k ? din + i * S : dout + (i - k) * S;
-    rsmi::MatArgs a = base_args(c, nullptr, 0, nullptr, 0, S, S, 1);
+    // The input is one stripe in the strided layout (shard j at din + j*S,
+    // parity t at dout + t*S): no shard table to upload, one launch, and a
+    // polled completion (rsmi::wait_event).
+    (void)n;
+    rsmi::MatArgs a = base_args(c, reinterpret_cast<void*>(din), 0, reinterpret_cast<void*>(dout), 0, S, S, 1);
     set_patterns(c, 1, c->d_encpat.p, a);
     a.stripe_desc = nullptr;
-    a.shard_ptrs = static_cast<const uint64_t*>(L.d_pieces.p);
-    hipError_t e = hipMemcpyAsync(L.d_pieces.p, tab, n * sizeof(uint64_t), hipMemcpyHostToDevice, s);
-    L.st_pieces.release_after(s);
-    if (e == hipSuccess) e = rsmi::launch_matmul(a, c->m, s);
-    const hipError_t sy = hipStreamSynchronize(s);
+    hipError_t e = launch_encode(c, a, s);
     L.end(s);
+    const hipError_t sy = e == hipSuccess ? rsmi::wait_event(L.dev_done) : hipSuccess;
     *rc = (e == hipSuccess && sy == hipSuccess) ? RS_OK : RS_EDEVICE;
     ++c->encodes_in_place;
     return true;
