@@ -10,7 +10,12 @@ namespace rsmi {
 
 namespace {
 constexpr size_t kPart = size_t(1) << 20;          // memcpy split granularity
-constexpr size_t kGroup = size_t(64) << 10;        // small pieces are handed out in runs of this many bytes
+// Bytes a helper thread must get to be worth waking: handing a part to a
+// sleeping worker costs tens of microseconds (futex wake, the queue lock), a
+// 1 MiB memcpy on one core 12-60 us; jobs below 2 parts' worth run inline on
+// the caller, larger ones are split in parts of at least this size
+// (RSMI_COPY_PART_MIN overrides).
+constexpr size_t kPartMin = size_t(1) << 20;
 constexpr size_t kChunkBytes = size_t(8) << 20;    // survivor bytes staged per chunk
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -98,6 +103,19 @@ void CopyPool::worker() {
 }
 
 void CopyPool::run(const std::vector<Piece>& pieces) {
+    static const size_t part_min = [] {
+        const char* e = std::getenv("RSMI_COPY_PART_MIN");
+        const long long v = e ? std::atoll(e) : 0;
+        return v > 0 ? static_cast<size_t>(v) : kPartMin;
+    }();
+    size_t total = 0;
+    for (const Piece& p : pieces) total += p.len;
+    if (total < 2 * part_min || threads_.empty()) {  // not worth a hand-off
+        for (const Piece& p : pieces) std::memcpy(p.dst, p.src, p.len);
+        return;
+    }
+    // Parts of about total / (2 x threads), at least part_min bytes.
+    const size_t group_bytes = std::max(part_min, total / (2 * (threads_.size() + 1)));
     Job job;
     size_t group = 0;  // bytes in the part being grouped
     job.bounds.push_back(0);
@@ -106,7 +124,7 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
             const size_t len = std::min(kPart, p.len - o);
             job.pieces.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o, len});
             group += len;
-            if (group >= kGroup) {
+            if (group >= group_bytes) {
                 job.bounds.push_back(job.pieces.size());
                 group = 0;
             }

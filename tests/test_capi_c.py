@@ -26,14 +26,17 @@ def test_abi_check_runs_on_gpu():
     assert "abi_check: ok" in r.stdout
 
 
-@pytest.mark.parametrize("spin_us", ["0", "200"])
+@pytest.mark.parametrize("spin_us,part_min", [("0", "0"), ("200", "65536")])
 @pytest.mark.parametrize("variant,iters", [("copypool_tsan", 3), ("copypool_asan", 20)])
-def test_copy_pool_concurrent_callers_under_sanitizer(variant, iters, spin_us):
-    """Also with the workers' spin phase (RSMI_COPY_SPIN_US): the lock-free
-    job counter they poll must not race the queue they then lock."""
+def test_copy_pool_concurrent_callers_under_sanitizer(variant, iters, spin_us, part_min):
+    """Also with the workers' spin phase (RSMI_COPY_SPIN_US: the lock-free
+    job counter they poll must not race the queue they then lock) and with
+    64 KiB parts (RSMI_COPY_PART_MIN: many small hand-offs)."""
     exe = os.path.join(BUILD, variant)
     assert os.path.exists(exe), "run __graft_entry__.build() (make -C tests/capi)"
     env = dict(os.environ, RSMI_COPY_THREADS="8", RSMI_COPY_SPIN_US=spin_us)
+    if part_min != "0":
+        env["RSMI_COPY_PART_MIN"] = part_min
     r = subprocess.run([exe, str(iters), "8"], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "copypool_stress: ok" in r.stdout

@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 passes of ONE default bench.py line (headline +
+config1 + config5 legs; tools/gpu/r04*.sh layout):
+
+  <dir>/trace/run_kernel_trace.csv   --kernel-trace --stats
+  <dir>/fetch/run_counter_collection.csv, <dir>/write/...   --pmc FETCH_SIZE / WRITE_SIZE (optional)
+
+Launches are told apart by kernel and grid size:
+  headline   rs_matmul_kernel launches with the largest grid, in launch order
+             alternating encode / reconstruct (bench.py --mode both);
+  config1    the other rs_matmul_kernel launches (one 1,048,580-byte message
+             per launch: 10 x 104,858-byte shards);
+  config5    rs_bitslice_k64_m16 (encode) and rs_bitslice_rec_k64_m16
+             (reconstruct), invert_patterns_kernel (the fresh patterns).
+HBM traffic per launch = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 (the gfx950
+correction of /opt/skills/guides/MI355X_MICROARCH.md), matched to the trace's
+roles by launch order within each kernel.  Writes markdown to <out> and, with
+--traffic-json, the headline's per-launch traffic for bench.py's
+roofline.traffic.
+
+usage: tools/prof_line.py <dir> <out.md> [--bench-json line.json] [--traffic-json profiles/traffic.json]
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+
+def rows(path):
+    if not os.path.exists(path):
+        return []
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def ms(r):
+    return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+
+
+def grid(r):
+    return int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
+
+
+def short(name):
+    for key in ("rs_bitslice_rec_k", "rs_bitslice_k", "rs_matmul_kernel", "invert_patterns_kernel"):
+        if key in name:
+            rest = name[name.index(key):]
+            return rest.split("(")[0] if key != "rs_matmul_kernel" else rest.split(">")[0] + ">"
+    return name[:40]
+
+
+def roles(trace):
+    """{role: [trace rows]} in launch order."""
+    mm = [r for r in trace if "rs_matmul_kernel" in r["Kernel_Name"]]
+    big = max((grid(r) for r in mm), default=0)
+    head = [r for r in mm if grid(r) == big]
+    out = {"headline encode": head[0::2], "headline reconstruct": head[1::2],
+           "config1 (one message per launch)": [r for r in mm if grid(r) != big],
+           "config5 encode": [r for r in trace if "rs_bitslice_k64_m16" in r["Kernel_Name"]],
+           "config5 reconstruct": [r for r in trace if "rs_bitslice_rec_k64_m16" in r["Kernel_Name"]],
+           "pattern builds": [r for r in trace if "invert_patterns_kernel" in r["Kernel_Name"]]}
+    return {k: v for k, v in out.items() if v}
+
+
+def pmc_by_role(d, counter):
+    """Counter values per role, matching the trace's classification: the
+    counter rows carry the grid size too."""
+    rs = [r for r in rows(os.path.join(d, counter.lower().split("_")[0], "run_counter_collection.csv"))
+          if r["Counter_Name"] == counter]
+    if not rs:
+        return {}
+    return {k: [float(r["Counter_Value"]) for r in v] for k, v in roles(rs).items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("out")
+    ap.add_argument("--bench-json", default=None)
+    ap.add_argument("--traffic-json", default=None)
+    a = ap.parse_args()
+    trace = rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv"))
+    rl = roles(trace)
+    fetch = pmc_by_role(a.dir, "FETCH_SIZE")
+    write = pmc_by_role(a.dir, "WRITE_SIZE")
+    b = json.load(open(a.bench_json)) if a.bench_json and os.path.exists(a.bench_json) else None
+    # algorithmic bytes per launch
+    alg = {"headline encode": 6553 * 14 * (1 << 20),
+           "headline reconstruct": 6553 * (10 + 2.5) * (1 << 20),   # E[e] = 2.5 for 1..4 uniform
+           "config1 (one message per launch)": None,
+           "config5 encode": 16384 * 80 * 65536,
+           "config5 reconstruct": 16384 * (64 + 8.5) * 65536}       # E[e] = 8.5 for 1..16 uniform
+    if b and "config" in b:
+        c = b["config"]
+        alg["headline encode"] = c["stripes_per_gpu"] * c["n"] * c["shard_bytes"]
+        alg["headline reconstruct"] = c["stripes_per_gpu"] * (c["k"] + (c["n"] - c["k"] + 1) / 2) * c["shard_bytes"]
+    if b and isinstance(b.get("config5"), dict) and b["config5"].get("status") == "ok":
+        alg["config5 encode"] = b["config5"]["encode"]["bytes"]
+        alg["config5 reconstruct"] = b["config5"]["reconstruct"]["bytes"]
+    lines = [f"# rocprofv3 summary of one bench.py line: {os.path.basename(os.path.normpath(a.dir))}", "",
+             "Kernel trace (`--kernel-trace --stats`) plus, when present, separate `--pmc FETCH_SIZE` and "
+             "`--pmc WRITE_SIZE` passes of the same command; traffic = FETCH_SIZE x 2 + WRITE_SIZE (gfx950 "
+             "correction, MI355X_MICROARCH §HBM).  Reconstruct algorithmic bytes are the expectation over the "
+             "uniform erasure counts (each profiled launch drew its own sets).", "",
+             "| role | kernel | launches | avg ms | algorithmic GB / launch | achieved GB/s | frac of 8 TB/s | "
+             "traffic GB / launch | traffic / algorithmic |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    traffic = {}
+    for role, rs in rl.items():
+        d = [ms(r) for r in rs]
+        avg = statistics.mean(d)
+        kern = short(rs[0]["Kernel_Name"])
+        al = alg.get(role)
+        f, w = fetch.get(role), write.get(role)
+        tr = (statistics.mean(f) * 2 + statistics.mean(w)) * 1024 / 1e9 if f and w else None
+        ach = al / (avg / 1e3) / 1e9 if al else None
+        lines.append(f"| {role} | `{kern}` | {len(d)} | {avg:.3f} | "
+                     f"{al / 1e9 if al else float('nan'):.2f} | {ach if ach else float('nan'):.0f} | "
+                     f"{ach / 8000 if ach else float('nan'):.4f} | {tr if tr is not None else float('nan'):.3f} | "
+                     f"{tr / (al / 1e9) if (tr is not None and al) else float('nan'):.3f} |")
+        if role == "headline encode" and tr is not None and b:
+            c = b["config"]
+            traffic[f"encode_k{c['k']}_n{c['n']}_S{c['shard_bytes']}_stripes{c['stripes_per_gpu']}"] = round(tr, 3)
+    lines.append("")
+    stats = rows(os.path.join(a.dir, "trace", "run_kernel_stats.csv"))
+    if stats:
+        lines += ["## rocprofv3 --stats (all launches of the line)", "",
+                  "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
+        for r in stats:
+            lines.append(f"| `{r['Name'][:80]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | "
+                         f"{float(r['MinNs']) / 1e6:.3f} | {float(r['MaxNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} |")
+        lines.append("")
+    if b:
+        lines.append(f"bench.py line of the profiled run: value {b['value']} GB/s, encode {b['breakdown']['encode_ms']} ms "
+                     f"(HIP events, frac {b['roofline']['frac']}), reconstruct {b['breakdown']['reconstruct_ms']} ms"
+                     + (f"; config5 encode {b['config5']['encode']['ms']} / reconstruct {b['config5']['reconstruct']['ms']} ms"
+                        if isinstance(b.get("config5"), dict) and b["config5"].get("status") == "ok" else "")
+                     + (f"; config1 encode {b['config1']['codec']['encode_ms']} / decode {b['config1']['codec']['decode4_ms']} ms"
+                        if isinstance(b.get("config1"), dict) and b["config1"].get("status") == "ok" else "") + ".")
+    with open(a.out, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    if a.traffic_json and traffic:
+        old = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
+        old.update(traffic)
+        json.dump(old, open(a.traffic_json, "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
