@@ -20,15 +20,19 @@ Also reported: the roofline of the dominant kernel (encode, HIP events on the
 launch stream) against the 8 TB/s HBM3E peak, and the CPU baseline (the
 oracle's ports of infectious's scalar and split-nibble addmul, 1 thread and
 all usable CPUs, on a bounded sample of the same workload, on rank 0 after
-the timed region at every N).
+the timed region at every N).  At N = 1 two more legs follow, never part of
+value: "config1" (configs[0], the reference's one-call-per-message pattern on
+the 1,048,580-byte blob, median latencies next to the oracle on one core) and
+"config5" (configs[4], RS(64,16) with 64 KiB shards, fresh 1-16 erasures).
 
 `--gpus N` with N > 1 and no launcher starts N ranks itself
 (torch.distributed.run as a child process, the JSON line relayed); under a
 launcher, WORLD_SIZE must equal --gpus.  At N > 1 the same ranks then run a
 short shard-distributed leg (configs[3]: the RCCL survivor gather and the
-pointer-mode reconstruct, checked on a sample) reported as "gather" -- never
-part of value, and abandoned by a per-rank watchdog rather than allowed to
-cost the headline line.
+pointer-mode reconstruct, the last two steps checked on a sample) reported
+as "gather" -- never part of value.  A per-rank watchdog abandons a leg stuck
+in a collective: the headline line is still printed, then the ranks exit
+with EXIT_GATHER_ABANDONED (75), so a hung gather never reads as success.
 """
 from __future__ import annotations
 

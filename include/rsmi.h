@@ -84,7 +84,10 @@ const char *rs_kernel_name(const rs_ctx *ctx, int which);
  * When input and parity are engine-pinned (rs_pinned_alloc / rs_arena),
  * 16-byte aligned with S % 16 == 0, and the code uses the split-table
  * kernel, the kernel reads and writes them in place over PCIe; rs_decode
- * likewise hands exactly-k engine-pinned survivors to rs_decode_batch. */
+ * likewise reads exactly k engine-pinned survivors in place (one launch, no
+ * staging; dst written in place too when it is engine-pinned).  Pageable
+ * buffers are staged through the lease's pinned memory, which the kernel
+ * reads and writes over PCIe. */
 int rs_encode(rs_ctx *ctx, const uint8_t *input, size_t len, uint8_t *parity);
 
 /* rs_decode replaces (*FEC).Decode(dst, shares) at main.go:77: Correct, then
@@ -172,6 +175,7 @@ enum {
     RS_STAT_BATCHES_STAGED = 3,    /* ... that staged them through pinned copies      */
     RS_STAT_LEASES = 4,            /* leases created (peak concurrent calls)          */
     RS_STAT_ENCODES_IN_PLACE = 5,  /* rs_encode calls served from engine-pinned memory */
+    RS_STAT_DECODES_IN_PLACE = 6,  /* rs_decode calls that read engine-pinned survivors in place */
 };
 int64_t rs_stat(const rs_ctx *ctx, int which);
 

@@ -208,6 +208,7 @@ struct Lease {
     Staging st_stripe;                 // stripe descriptors
     Staging st_batch, st_pieces;       // rs_decode_batch
     Staging st_onepat;                 // host-API decode: the one-pattern table, read in place by the kernel
+    Staging st_out;                    // decode_in_place: regenerated shares when dst is not engine-pinned
     DevBuf d_stripe_pat, d_batch, d_pack, d_pieces, d_onepat;
     std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
     std::vector<uint32_t> pid, start;          // reconstruct scratch
@@ -248,6 +249,7 @@ struct Lease {
         st_batch.destroy();
         st_pieces.destroy();
         st_onepat.destroy();
+        st_out.destroy();
         for (DevBuf* b : {&d_stripe_pat, &d_batch, &d_pack, &d_pieces, &d_onepat}) b->release();
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -299,6 +301,7 @@ struct rs_ctx {
     uint64_t tables_gen = 0;  // bumped when the device tables move (growth) or are rebuilt (eviction)
     std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
     std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
+    std::atomic<int64_t> decodes_in_place{0};                     // rs_decode from engine-pinned memory
     hipEvent_t pat_ev = nullptr;
     hipStream_t build_stream = nullptr;  // pattern builds (flush_patterns), off every caller's stream
     hipEvent_t caller_ev = nullptr;      // the building caller's stream tail (build_after_caller)
@@ -1006,6 +1009,100 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
     return true;
 }
 
+// rs_decode of exactly k distinct shares that all lie in engine-pinned
+// memory (pinned.hpp: an rs_arena / rs_pinned_alloc range, 16-byte aligned,
+// readable up to round_up(S, 16)): the split-table kernel reads the
+// survivors over PCIe where they are, through a one-stripe shard table that
+// sits with the one-pattern table in the lease's pinned staging (read in
+// place too: nothing is uploaded).  The regenerated data shares go straight
+// into dst when dst is engine-pinned as well, else through pinned staging;
+// the present ones are copied into dst on the host while the kernel runs.
+// Returns false (nothing done) when the shares are not all engine-pinned.
+bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
+                     const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst, int* rc) {
+    const int k = c->k;
+    if (S == 0 || std::getenv("RSMI_NO_DIRECT")) return false;
+    const size_t span = round_up(S, 16);
+    std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
+    std::vector<uint64_t> dev(k);
+    for (int j = 0; j < k; ++j) {
+        const uint8_t* p = by_id[surv[j]];
+        if (reinterpret_cast<uintptr_t>(p) & 15u) return false;
+        dev[j] = rsmi::pinned_device_address(p, span);
+        if (!dev[j]) return false;
+    }
+    std::vector<int> missing;
+    for (int i = 0; i < k; ++i)
+        if (!present[i]) missing.push_back(i);
+    const int e = static_cast<int>(missing.size());
+    auto copy_present = [&] {
+        for (int i = 0; i < k; ++i)
+            if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
+    };
+    if (e == 0) {
+        copy_present();
+        *rc = RS_OK;
+        return true;
+    }
+    std::vector<uint8_t> rows;
+    if (!rsmi::decode_rows(c->enc, k, c->n, surv, missing, rows)) {
+        *rc = RS_ESINGULAR;
+        return true;
+    }
+    // Outputs: dst's rows in place when dst is engine-pinned (and the rows
+    // 16-byte aligned), else rows of the lease's pinned output staging.
+    const bool dst_direct = !(S & 15u) && !(reinterpret_cast<uintptr_t>(dst) & 15u) &&
+                            rsmi::pinned_device_address(dst, static_cast<size_t>(k) * S) != 0;
+    if (!dst_direct && !L.st_out.acquire(static_cast<size_t>(e) * span)) {
+        *rc = RS_ENOMEM;
+        return true;
+    }
+    // Pinned staging: [one-pattern table][shard table: k survivors, e outputs]
+    const size_t pbytes = PatLayout(c, 1).total, toff = round_up(pbytes, 16);
+    const size_t tbytes = toff + static_cast<size_t>(c->n) * 8;
+    if (!L.st_onepat.acquire(tbytes)) {
+        *rc = RS_ENOMEM;
+        return true;
+    }
+    uint8_t* host = static_cast<uint8_t*>(L.st_onepat.p);
+    std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
+    std::copy(rows.begin(), rows.end(), coef.begin());
+    std::vector<uint32_t> src(k), dstid(c->m, 0), cnt(1, static_cast<uint32_t>(e));
+    for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
+    for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
+    pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), host);
+    void* halias = nullptr;
+    if (hipHostGetDevicePointer(&halias, host, 0) != hipSuccess) halias = host;
+    uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff);
+    for (int j = 0; j < k; ++j) tab[j] = dev[j];
+    uint64_t oalias = 0;
+    if (!dst_direct) {
+        void* oa = nullptr;
+        if (hipHostGetDevicePointer(&oa, L.st_out.p, 0) != hipSuccess) oa = L.st_out.p;
+        oalias = reinterpret_cast<uint64_t>(oa);
+    }
+    for (int t = 0; t < e; ++t)
+        tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span)
+                                : oalias + static_cast<uint64_t>(t) * span;
+    const void* pat = halias;
+    rsmi::MatArgs a = base_args(c, nullptr, 0, nullptr, 0, span, S, 1);
+    set_patterns(c, 1, pat, a);
+    a.stripe_desc = first_stripe_desc(c, pat);
+    a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff);
+    const hipStream_t s = L.stream;
+    L.begin(s);
+    hipError_t err = rsmi::launch_matmul(a, e, s);
+    L.end(s);
+    copy_present();  // while the kernel runs
+    if (err == hipSuccess) err = rsmi::wait_event(L.dev_done);
+    if (err == hipSuccess && !dst_direct)
+        for (int t = 0; t < e; ++t)
+            std::memcpy(dst + static_cast<size_t>(missing[t]) * S, static_cast<uint8_t*>(L.st_out.p) + t * span, S);
+    *rc = err == hipSuccess ? RS_OK : RS_EDEVICE;
+    ++c->decodes_in_place;
+    return true;
+}
+
 // Rebuild from the present shares: data shares copied, missing ones
 // regenerated from Rebuild's survivors.
 int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
@@ -1424,6 +1521,7 @@ int64_t rs_stat(const rs_ctx* c, int which) {
         case RS_STAT_BATCHES_IN_PLACE: return c->batches_in_place.load();
         case RS_STAT_BATCHES_STAGED: return c->batches_staged.load();
         case RS_STAT_ENCODES_IN_PLACE: return c->encodes_in_place.load();
+        case RS_STAT_DECODES_IN_PLACE: return c->decodes_in_place.load();
         case RS_STAT_LEASES: {
             std::lock_guard<std::mutex> lk(const_cast<rs_ctx*>(c)->lease_mu);
             return static_cast<int64_t>(c->leases.size());
@@ -1611,27 +1709,15 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (share_len == 0) return RS_OK;
     for (int i = 0; i < n; ++i)
         if (present[i] && !by_id[i]) return RS_EINVAL;
-    // (below ~16 KiB shards the batch path's fixed costs outweigh the staging
-    // it saves: 64 KiB messages decode in 0.074 vs 0.063 ms, profiles/r02m)
-    if (distinct == k && count == k && share_len >= (size_t(16) << 10) && !std::getenv("RSMI_NO_DIRECT")) {
-        // Survivors in engine-pinned memory: one in-place reconstruct launch
-        // (rs_decode_batch reads them over PCIe without staging).
-        bool pinned = true;
-        for (int i = 0; i < count && pinned; ++i)
-            pinned = !(reinterpret_cast<uintptr_t>(ptrs[i]) & 15u) &&
-                     rsmi::pinned_device_address(ptrs[i], round_up(share_len, 16)) != 0;
-        if (pinned) {
-            int cnt = count, st = RS_OK;
-            uint8_t* d1 = dst;
-            const int rc = rs_decode_batch(c, 1, &cnt, numbers, shares, share_len, &d1, &st);
-            return rc != RS_OK ? rc : st;
-        }
-    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
     if (!lg.L) return RS_ENOMEM;
     if (distinct > k) return correct_decode(c, *lg.L, present, by_id, share_len, dst);
+    // Survivors in engine-pinned memory (an rs_arena, rs_pinned_alloc): one
+    // launch reads them in place, no staging copies.
+    int rc_in_place = RS_OK;
+    if (decode_in_place(c, *lg.L, present, by_id, share_len, dst, &rc_in_place)) return rc_in_place;
     return rebuild_into(c, *lg.L, present, by_id, share_len, dst);
 }
 

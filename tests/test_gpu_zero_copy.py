@@ -132,9 +132,10 @@ def test_unmarshal_into_arena_then_decode_in_place():
 def test_host_api_in_place_encode_decode(k, n, S):
     """rs_encode with input and parity in engine-pinned memory runs the
     split-table kernel on them in place (no staging); rs_decode of k pinned
-    survivors goes through the in-place batch path from 16 KiB shards up
-    (below that the staged pipeline is faster, rsmi.cpp rs_decode).  Bit-exact
-    vs oracle."""
+    survivors reads them in place too (rsmi.cpp decode_in_place: one launch,
+    pattern and shard table read from pinned staging), writing the missing
+    shares straight into a pinned dst or through staging into a pageable one.
+    Bit-exact vs oracle."""
     lib = rsmi.load()
     f = rsmi.FEC(k, n)
     m = n - k
@@ -149,11 +150,23 @@ def test_host_api_in_place_encode_decode(k, n, S):
         keep = list(range(m, k)) + list(range(k, n))  # first m data shards lost
         nums = (ctypes.c_int * k)(*keep[::-1])
         ptrs = (ctypes.c_void_p * k)(*[pin_in + i * S if i < k else pin_par + (i - k) * S for i in keep[::-1]])
-        b0 = f.stat(f.STAT_BATCHES_IN_PLACE)
+        d0 = f.stat(f.STAT_DECODES_IN_PLACE)
         assert lib.rs_decode(f.handle, nums, ptrs, k, S, pin_dst) == rsmi.RS_OK
-        assert f.stat(f.STAT_BATCHES_IN_PLACE) == b0 + (1 if S >= (16 << 10) else 0)
+        assert f.stat(f.STAT_DECODES_IN_PLACE) == d0 + 1
         assert ctypes.string_at(pin_dst, k * S) == data
         assert list(nums) == sorted(keep)
+        # pageable dst: the regenerated shares go through pinned staging
+        pdst = ctypes.create_string_buffer(k * S)
+        nums = (ctypes.c_int * k)(*keep)
+        ptrs = (ctypes.c_void_p * k)(*[pin_in + i * S if i < k else pin_par + (i - k) * S for i in keep])
+        assert lib.rs_decode(f.handle, nums, ptrs, k, S, ctypes.cast(pdst, ctypes.c_void_p)) == rsmi.RS_OK
+        assert f.stat(f.STAT_DECODES_IN_PLACE) == d0 + 2 and pdst.raw == data
+        # one survivor pageable: the staged path, same bytes
+        lone = ctypes.create_string_buffer(ctypes.string_at(ptrs[0], S), S)
+        ptrs[0] = ctypes.cast(lone, ctypes.c_void_p)
+        pdst2 = ctypes.create_string_buffer(k * S)
+        assert lib.rs_decode(f.handle, nums, ptrs, k, S, ctypes.cast(pdst2, ctypes.c_void_p)) == rsmi.RS_OK
+        assert f.stat(f.STAT_DECODES_IN_PLACE) == d0 + 2 and pdst2.raw == data
         # pageable parity: staged pipeline, same bytes
         pageable = ctypes.create_string_buffer(m * S)
         assert lib.rs_encode(f.handle, pin_in, k * S, ctypes.cast(pageable, ctypes.c_void_p)) == rsmi.RS_OK

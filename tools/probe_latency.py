@@ -7,6 +7,8 @@ not a bench line).  Medians over --reps calls of:
   encode_pinned     rs_encode with input and parity in engine-pinned memory
                     (16-byte shards: the kernel reads / writes them in place,
                     no staging copies) -- the GPU part alone
+  decode_pinned     rs_decode of 10 engine-pinned survivors into a pinned dst
+                    (read and written in place)
   launch_sync       an empty torch kernel + synchronize (launch + completion
                     latency floor)
   copy_1mib_1t      numpy copy of 1 MiB pageable -> pinned on one thread
@@ -72,6 +74,15 @@ def main():
     pin_in, pin_par = lib.rs_pinned_alloc(Sp * k), lib.rs_pinned_alloc(Sp * m)
     ctypes.memmove(pin_in, blob.ctypes.data, Sp * k)
     out["encode_pinned"] = med(lambda: lib.rs_encode(f.handle, pin_in, Sp * k, pin_par), a.reps)
+    pin_dst = lib.rs_pinned_alloc(Sp * k)
+
+    def pdec():
+        nums = (ctypes.c_int * k)(*keep)
+        ptrs = (ctypes.c_void_p * k)(*[pin_in + i * Sp if i < k else pin_par + (i - k) * Sp for i in keep])
+        assert lib.rs_decode(f.handle, nums, ptrs, k, Sp, pin_dst) == 0
+    out["decode_pinned"] = med(pdec, a.reps)
+    assert ctypes.string_at(pin_dst, Sp * k) == ctypes.string_at(pin_in, Sp * k)
+    lib.rs_pinned_free(pin_dst)
     x = torch.zeros(1, device="cuda")
 
     def ls():
