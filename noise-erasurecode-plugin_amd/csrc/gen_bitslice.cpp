@@ -82,6 +82,11 @@ bool kDebugMasks = false;
 // offset selects).  Same-box A/B, 10 steps x 2 (profiles/r04c/): config 5
 // reconstruct fresh 1-16 -1.7%, 16 erasures -1.1%, RS(8,14) -2.5%.
 bool kBufferLoads = true;
+// Reconstruct inputs enter through an opaque asm on their load registers
+// (default) so their transpose stays after the prefetch; -N drops it (the
+// vmcnt waits are unchanged, and hipcc then transposes in the load
+// registers instead of copying them out first).
+bool kInputBarrier = true;
 // Solve tail (-L): outputs past e in the last group of R are skipped by a
 // wave-uniform branch per (syndrome, output) instead of coded as padding;
 // the syndrome's bit fields are extracted once per group for all outputs.
@@ -507,9 +512,10 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
             emit_load(j + PF, (j + PF) % (PF + 1));
         std::fprintf(f, "    if (%s) {\n", pres(j).c_str());
         const std::string xb = "x[" + std::to_string(buf) + "]";
-        std::fprintf(f, "        asm volatile(\"\" : \"+v\"(%s[0]), \"+v\"(%s[1]), \"+v\"(%s[2]), \"+v\"(%s[3]), "
-                        "\"+v\"(%s[4]), \"+v\"(%s[5]), \"+v\"(%s[6]), \"+v\"(%s[7]));\n",
-                     xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str());
+        if (kInputBarrier)
+            std::fprintf(f, "        asm volatile(\"\" : \"+v\"(%s[0]), \"+v\"(%s[1]), \"+v\"(%s[2]), \"+v\"(%s[3]), "
+                            "\"+v\"(%s[4]), \"+v\"(%s[5]), \"+v\"(%s[6]), \"+v\"(%s[7]));\n",
+                         xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str(), xb.c_str());
         if (kMovementOnly) {
             // movement twin: the input only enters one row's accumulators
             const int t = (j % top) * 8;
@@ -778,6 +784,11 @@ int main(int argc, char** argv) {
         argv += 1;
         argc -= 1;
     }
+    if (argc >= 2 && std::string(argv[1]) == "-N") {
+        kInputBarrier = false;
+        argv += 1;
+        argc -= 1;
+    }
     if (argc >= 2 && std::string(argv[1]) == "-L") {
         kSolveTail = true;
         argv += 1;
@@ -822,7 +833,7 @@ int main(int argc, char** argv) {
         argc -= 2;
     }
     if (argc < 3) {
-        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
         return 2;
     }
     std::vector<std::pair<int, int>> codes;
