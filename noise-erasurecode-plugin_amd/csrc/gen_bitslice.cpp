@@ -82,11 +82,13 @@ bool kDebugMasks = false;
 // offset selects).  Same-box A/B, 10 steps x 2 (profiles/r04c/): config 5
 // reconstruct fresh 1-16 -1.7%, 16 erasures -1.1%, RS(8,14) -2.5%.
 bool kBufferLoads = true;
-// Reconstruct inputs enter through an opaque asm on their load registers
-// (default) so their transpose stays after the prefetch; -N drops it (the
-// vmcnt waits are unchanged, and hipcc then transposes in the load
-// registers instead of copying them out first).
-bool kInputBarrier = true;
+// Reconstruct inputs entered through an opaque asm on their load registers
+// (round 3; -Y restores it) so their transpose stayed after the prefetch.
+// Without it (default) the vmcnt waits are unchanged and hipcc transposes in
+// the load registers instead of copying them out first: 264 fewer VALU in
+// the RS(64,16) kernel's ISA, same-box A/B 10 steps x 2 (profiles/r04h/):
+// config 5 fresh -0.4..-0.9%, pool -0.4..-0.8%, 16 erasures -0.1%.
+bool kInputBarrier = false;
 // Solve tail (-L): outputs past e in the last group of R are skipped by a
 // wave-uniform branch per (syndrome, output) instead of coded as padding;
 // the syndrome's bit fields are extracted once per group for all outputs.
@@ -789,6 +791,11 @@ int main(int argc, char** argv) {
         argv += 1;
         argc -= 1;
     }
+    if (argc >= 2 && std::string(argv[1]) == "-Y") {
+        kInputBarrier = true;
+        argv += 1;
+        argc -= 1;
+    }
     if (argc >= 2 && std::string(argv[1]) == "-L") {
         kSolveTail = true;
         argv += 1;
@@ -833,7 +840,7 @@ int main(int argc, char** argv) {
         argc -= 2;
     }
     if (argc < 3) {
-        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N|-Y] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
         return 2;
     }
     std::vector<std::pair<int, int>> codes;
