@@ -209,6 +209,7 @@ struct Lease {
     Staging st_batch, st_pieces;       // rs_decode_batch
     Staging st_onepat;                 // host-API decode: the one-pattern table, read in place by the kernel
     Staging st_out;                    // decode_in_place: regenerated shares when dst is not engine-pinned
+    Staging st_in;                     // decode_staged / encode_staged: a small message's survivors
     DevBuf d_stripe_pat, d_batch, d_pack, d_pieces, d_onepat;
     std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
     std::vector<uint32_t> pid, start;          // reconstruct scratch
@@ -250,6 +251,7 @@ struct Lease {
         st_pieces.destroy();
         st_onepat.destroy();
         st_out.destroy();
+        st_in.destroy();
         for (DevBuf* b : {&d_stripe_pat, &d_batch, &d_pack, &d_pieces, &d_onepat}) b->release();
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -1018,6 +1020,13 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
 // into dst when dst is engine-pinned as well, else through pinned staging;
 // the present ones are copied into dst on the host while the kernel runs.
 // Returns false (nothing done) when the shares are not all engine-pinned.
+// The one-launch decode of decode_in_place / decode_staged: survivor j of
+// Rebuild's choice `surv` is read at device address dev[j]; the present data
+// shares are copied into dst (unless present_done) while the kernel runs.
+int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
+                  const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
+                  bool present_done);
+
 bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
                      const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst, int* rc) {
     const int k = c->k;
@@ -1031,39 +1040,68 @@ bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
         dev[j] = rsmi::pinned_device_address(p, span);
         if (!dev[j]) return false;
     }
+    *rc = decode_launch(c, L, present, by_id, surv, dev, S, dst, false);
+    ++c->decodes_in_place;
+    return true;
+}
+
+// A message whose k survivors fit the one-shot staging (kStageSmall, the copy
+// pool's inline threshold, host_pipeline.cpp):
+// each survivor is copied into pinned staging once -- a present data share
+// also into dst right after, while its bytes are in cache -- and the
+// one-launch decode reads the staging in place.  Larger messages take the
+// chunked pipeline (host_pipeline.cpp), whose copies overlap its chunks.
+constexpr size_t kStageSmall = size_t(2) << 20;
+
+bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
+                   size_t S, uint8_t* dst, int* rc) {
+    const int k = c->k;
+    const size_t span = round_up(S, 16);
+    if (S == 0 || static_cast<size_t>(k) * span > kStageSmall || std::getenv("RSMI_NO_STAGE_SMALL")) return false;
+    if (!L.st_in.acquire(static_cast<size_t>(k) * span)) return false;
+    void* alias = nullptr;
+    if (hipHostGetDevicePointer(&alias, L.st_in.p, 0) != hipSuccess) alias = L.st_in.p;
+    std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
+    std::vector<uint64_t> dev(k);
+    uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
+    for (int j = 0; j < k; ++j) {
+        std::memcpy(st + static_cast<size_t>(j) * span, by_id[surv[j]], S);
+        if (surv[j] < k) std::memcpy(dst + static_cast<size_t>(surv[j]) * S, by_id[surv[j]], S);
+        dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
+    }
+    *rc = decode_launch(c, L, present, by_id, surv, dev, S, dst, true);
+    return true;
+}
+
+int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
+                  const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
+                  bool present_done) {
+    const int k = c->k;
+    const size_t span = round_up(S, 16);
     std::vector<int> missing;
     for (int i = 0; i < k; ++i)
         if (!present[i]) missing.push_back(i);
     const int e = static_cast<int>(missing.size());
     auto copy_present = [&] {
+        if (present_done) return;
         for (int i = 0; i < k; ++i)
             if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
     };
     if (e == 0) {
         copy_present();
-        *rc = RS_OK;
-        return true;
+        return RS_OK;
     }
     std::vector<uint8_t> rows;
-    if (!rsmi::decode_rows(c->enc, k, c->n, surv, missing, rows)) {
-        *rc = RS_ESINGULAR;
-        return true;
-    }
+    if (!rsmi::decode_rows(c->enc, k, c->n, surv, missing, rows)) return RS_ESINGULAR;
     // Outputs: dst's rows in place when dst is engine-pinned (and the rows
     // 16-byte aligned), else rows of the lease's pinned output staging.
     const bool dst_direct = !(S & 15u) && !(reinterpret_cast<uintptr_t>(dst) & 15u) &&
                             rsmi::pinned_device_address(dst, static_cast<size_t>(k) * S) != 0;
-    if (!dst_direct && !L.st_out.acquire(static_cast<size_t>(e) * span)) {
-        *rc = RS_ENOMEM;
-        return true;
-    }
+    if (!dst_direct && !L.st_out.acquire(static_cast<size_t>(e) * span)) return RS_ENOMEM;
     // Pinned staging: [one-pattern table][shard table: k survivors, e outputs]
     const size_t pbytes = PatLayout(c, 1).total, toff = round_up(pbytes, 16);
     const size_t tbytes = toff + static_cast<size_t>(c->n) * 8;
-    if (!L.st_onepat.acquire(tbytes)) {
-        *rc = RS_ENOMEM;
-        return true;
-    }
+    if (!L.st_onepat.acquire(tbytes)) return RS_ENOMEM;
     uint8_t* host = static_cast<uint8_t*>(L.st_onepat.p);
     std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
     std::copy(rows.begin(), rows.end(), coef.begin());
@@ -1098,8 +1136,43 @@ bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
     if (err == hipSuccess && !dst_direct)
         for (int t = 0; t < e; ++t)
             std::memcpy(dst + static_cast<size_t>(missing[t]) * S, static_cast<uint8_t*>(L.st_out.p) + t * span, S);
-    *rc = err == hipSuccess ? RS_OK : RS_EDEVICE;
-    ++c->decodes_in_place;
+    return err == hipSuccess ? RS_OK : RS_EDEVICE;
+}
+
+// rs_encode of a small message (k shards within kStageSmall) from pageable
+// buffers: the input is copied once into pinned staging in the strided
+// layout (pitch round_up(S, 16)), one encode launch reads it and writes the
+// parity into pinned staging over PCIe, and the parity rows are copied out.
+bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t* parity, int* rc) {
+    const size_t k = c->k, m = c->m, span = round_up(S, 16);
+    if (S == 0 || k * span > kStageSmall || std::getenv("RSMI_NO_STAGE_SMALL")) return false;
+    if (!L.st_in.acquire(k * span) || !L.st_out.acquire(m * span)) return false;
+    void *din = nullptr, *dout = nullptr;
+    if (hipHostGetDevicePointer(&din, L.st_in.p, 0) != hipSuccess) din = L.st_in.p;
+    if (hipHostGetDevicePointer(&dout, L.st_out.p, 0) != hipSuccess) dout = L.st_out.p;
+    uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
+    if (span == S) {
+        std::memcpy(st, input, k * S);
+    } else {
+        for (size_t j = 0; j < k; ++j) std::memcpy(st + j * span, input + j * S, S);
+    }
+    const hipStream_t s = L.stream;
+    L.begin(s);
+    rsmi::MatArgs a = base_args(c, din, 0, dout, 0, span, S, 1);
+    set_patterns(c, 1, c->d_encpat.p, a);
+    a.stripe_desc = nullptr;
+    hipError_t e = launch_encode(c, a, s);
+    L.end(s);
+    if (e == hipSuccess) e = rsmi::wait_event(L.dev_done);
+    if (e == hipSuccess) {
+        const uint8_t* out = static_cast<const uint8_t*>(L.st_out.p);
+        if (span == S) {
+            std::memcpy(parity, out, m * S);
+        } else {
+            for (size_t t = 0; t < m; ++t) std::memcpy(parity + t * S, out + t * span, S);
+        }
+    }
+    *rc = e == hipSuccess ? RS_OK : RS_EDEVICE;
     return true;
 }
 
@@ -1108,6 +1181,8 @@ bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
 int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
                  const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst) {
     const int k = c->k;
+    int rc_small = RS_OK;
+    if (decode_staged(c, L, present, by_id, S, dst, &rc_small)) return rc_small;
     std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
     std::vector<const uint8_t*> sp(k);
     for (int i = 0; i < k; ++i) sp[i] = by_id[surv[i]];
@@ -1661,6 +1736,7 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     if (!lg.L) return RS_ENOMEM;
     int rc_in_place = RS_OK;
     if (encode_in_place(c, *lg.L, input, S, parity, &rc_in_place)) return rc_in_place;
+    if (encode_staged(c, *lg.L, input, S, parity, &rc_in_place)) return rc_in_place;
     rsmi::HostPipeline* pipe = lg.L->pipeline();
     if (!pipe) return RS_ENOMEM;
     std::vector<const uint8_t*> srcs(c->k);
