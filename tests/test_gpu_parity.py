@@ -1031,3 +1031,37 @@ def test_xcd_block_order_matches_natural(k, n, S, stripes):
         assert torch.equal(data, d0) and torch.equal(parity, p0), name
     for f in fx.values():
         f.close()
+
+
+@pytest.mark.parametrize("S", [209_700, 209_716, 209_733, 2 * 1024 * 1024 + 5])
+@pytest.mark.parametrize("stage_small", [True, False])
+def test_host_api_staging_threshold(S, stage_small, monkeypatch):
+    """rs_encode / rs_decode on pageable buffers around the one-shot staging
+    threshold (k x round_up(S, 16) <= 2 MiB: staged once and coded by one
+    launch, rsmi.cpp encode_staged / decode_staged) and past it (the chunked
+    pipeline, several 8 MiB chunks at S = 2 MiB + 5), unaligned shard
+    lengths included; RSMI_NO_STAGE_SMALL forces the pipeline for the small
+    sizes too.  Bit-exact vs the oracle; decode with 4 drops including
+    parity."""
+    import ctypes
+    if not stage_small:
+        monkeypatch.setenv("RSMI_NO_STAGE_SMALL", "1")
+    k, n = 10, 14
+    m = n - k
+    f = fec(k, n)
+    lib = rsmi.load()
+    E = oracle.fec_matrix(k, n)
+    data = oracle.splitmix_bytes(k * S, S + 17)
+    par = np.zeros(m * S, dtype=np.uint8)
+    P = ctypes.c_void_p
+    assert lib.rs_encode(f.handle, P(data.ctypes.data), k * S, P(par.ctypes.data)) == 0
+    assert par.tobytes() == oracle.encode(E, k, n, data.tobytes())
+    shard = lambda i: data[i * S:(i + 1) * S] if i < k else par[(i - k) * S:(i - k + 1) * S]
+    for lost in ((0, 3, 7, 12), (1, 2, 10, 11), (9, 10, 11, 13)):
+        keep = [i for i in range(n) if i not in lost]
+        bufs = [np.ascontiguousarray(shard(i)) for i in keep]
+        dst = np.zeros(k * S, dtype=np.uint8)
+        nums = (ctypes.c_int * k)(*keep[::-1])
+        ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs[::-1]])
+        assert lib.rs_decode(f.handle, nums, ptrs, k, S, P(dst.ctypes.data)) == 0
+        assert np.array_equal(dst, data), lost
