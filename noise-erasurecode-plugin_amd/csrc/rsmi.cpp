@@ -1023,9 +1023,25 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
 // Rebuild's choice `surv` is read at device address dev[j]; the present data
 // shares are copied into dst (unless present_done) while the kernel runs.
+using StageFn = std::function<void(size_t off, size_t w)>;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
-                  bool present_done);
+                  bool present_done, int nch = 1, const StageFn& stage = nullptr);
+
+// Column chunks of a staged small message: chunk c covers bytes
+// [off(c), off(c + 1)) of every shard, offsets multiples of 16.  Two chunks
+// let the host stage the second half while the kernel codes the first (and
+// copy the first half's outputs out while it codes the second);
+// RSMI_STAGE_CHUNKS overrides (1..4).
+int stage_chunks(size_t bytes) {
+    static const int forced = [] {
+        const char* e = std::getenv("RSMI_STAGE_CHUNKS");
+        return e ? std::max(1, std::min(std::atoi(e), 4)) : 0;
+    }();
+    if (forced) return forced;
+    return bytes >= (size_t(256) << 10) ? 2 : 1;
+}
+size_t chunk_off(size_t S, int c, int nch) { return c >= nch ? S : (S * c / nch) & ~size_t(15); }
 
 bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
                      const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst, int* rc) {
@@ -1065,17 +1081,19 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
     std::vector<uint64_t> dev(k);
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
-    for (int j = 0; j < k; ++j) {
-        std::memcpy(st + static_cast<size_t>(j) * span, by_id[surv[j]], S);
-        dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
-    }
-    *rc = decode_launch(c, L, present, by_id, surv, dev, S, dst, false);
+    for (int j = 0; j < k; ++j) dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
+    // survivors' columns [off, off + w) into staging, chunk by chunk
+    auto stage = [&](size_t off, size_t w) {
+        for (int j = 0; j < k; ++j) std::memcpy(st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w);
+    };
+    *rc = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
+                        stage_chunks(static_cast<size_t>(k) * S), stage);
     return true;
 }
 
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
-                  bool present_done) {
+                  bool present_done, int nch, const StageFn& stage) {
     const int k = c->k;
     const size_t span = round_up(S, 16);
     std::vector<int> missing;
@@ -1093,15 +1111,16 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     }
     std::vector<uint8_t> rows;
     if (!rsmi::decode_rows(c->enc, k, c->n, surv, missing, rows)) return RS_ESINGULAR;
+    nch = std::max(1, std::min(nch, static_cast<int>(std::min<size_t>(kBatchChunks, S / 4096))));  // >= 4 KiB a chunk
     // Outputs: dst's rows in place when dst is engine-pinned (and the rows
     // 16-byte aligned), else rows of the lease's pinned output staging.
     const bool dst_direct = !(S & 15u) && !(reinterpret_cast<uintptr_t>(dst) & 15u) &&
                             rsmi::pinned_device_address(dst, static_cast<size_t>(k) * S) != 0;
     if (!dst_direct && !L.st_out.acquire(static_cast<size_t>(e) * span)) return RS_ENOMEM;
-    // Pinned staging: [one-pattern table][shard table: k survivors, e outputs]
+    // Pinned staging: [one-pattern table][nch shard tables: k survivors, e outputs]
     const size_t pbytes = PatLayout(c, 1).total, toff = round_up(pbytes, 16);
-    const size_t tbytes = toff + static_cast<size_t>(c->n) * 8;
-    if (!L.st_onepat.acquire(tbytes)) return RS_ENOMEM;
+    const size_t n8 = static_cast<size_t>(c->n) * 8;
+    if (!L.st_onepat.acquire(toff + nch * n8)) return RS_ENOMEM;
     uint8_t* host = static_cast<uint8_t*>(L.st_onepat.p);
     std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
     std::copy(rows.begin(), rows.end(), coef.begin());
@@ -1111,31 +1130,45 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), host);
     void* halias = nullptr;
     if (hipHostGetDevicePointer(&halias, host, 0) != hipSuccess) halias = host;
-    uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff);
-    for (int j = 0; j < k; ++j) tab[j] = dev[j];
     uint64_t oalias = 0;
     if (!dst_direct) {
         void* oa = nullptr;
         if (hipHostGetDevicePointer(&oa, L.st_out.p, 0) != hipSuccess) oa = L.st_out.p;
         oalias = reinterpret_cast<uint64_t>(oa);
     }
-    for (int t = 0; t < e; ++t)
-        tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span)
-                                : oalias + static_cast<uint64_t>(t) * span;
     const void* pat = halias;
-    rsmi::MatArgs a = base_args(c, nullptr, 0, nullptr, 0, span, S, 1);
-    set_patterns(c, 1, pat, a);
-    a.stripe_desc = first_stripe_desc(c, pat);
-    a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff);
     const hipStream_t s = L.stream;
     L.begin(s);
-    hipError_t err = rsmi::launch_matmul(a, e, s);
+    hipError_t err = hipSuccess;
+    int launched = 0;
+    for (int ch = 0; ch < nch && err == hipSuccess; ++ch) {
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        if (stage) stage(off, w);
+        uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff + ch * n8);
+        for (int jj = 0; jj < k; ++jj) tab[jj] = dev[jj] + off;
+        for (int t = 0; t < e; ++t)
+            tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span) + off
+                                    : oalias + static_cast<uint64_t>(t) * span + off;
+        rsmi::MatArgs a = base_args(c, nullptr, 0, nullptr, 0, span, w, 1);
+        set_patterns(c, 1, pat, a);
+        a.stripe_desc = first_stripe_desc(c, pat);
+        a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
+        err = rsmi::launch_matmul(a, e, s);
+        if (err == hipSuccess) err = hipEventRecord(L.ev[ch], s);
+        if (err == hipSuccess) ++launched;
+    }
     L.end(s);
     copy_present();  // while the kernel runs
-    if (err == hipSuccess) err = rsmi::wait_event(L.dev_done);
-    if (err == hipSuccess && !dst_direct)
+    for (int ch = 0; ch < launched; ++ch) {
+        const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
+        if (err == hipSuccess) err = w8;
+        if (err != hipSuccess || dst_direct) continue;
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
         for (int t = 0; t < e; ++t)
-            std::memcpy(dst + static_cast<size_t>(missing[t]) * S, static_cast<uint8_t*>(L.st_out.p) + t * span, S);
+            std::memcpy(dst + static_cast<size_t>(missing[t]) * S + off,
+                        static_cast<uint8_t*>(L.st_out.p) + t * span + off, w);
+    }
+    if (launched < nch) (void)rsmi::wait_event(L.dev_done);  // a failed launch: drain what was queued
     return err == hipSuccess ? RS_OK : RS_EDEVICE;
 }
 
@@ -1151,27 +1184,32 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
     if (hipHostGetDevicePointer(&din, L.st_in.p, 0) != hipSuccess) din = L.st_in.p;
     if (hipHostGetDevicePointer(&dout, L.st_out.p, 0) != hipSuccess) dout = L.st_out.p;
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
-    if (span == S) {
-        std::memcpy(st, input, k * S);
-    } else {
-        for (size_t j = 0; j < k; ++j) std::memcpy(st + j * span, input + j * S, S);
-    }
+    const uint8_t* out = static_cast<const uint8_t*>(L.st_out.p);
+    const int nch = std::max(1, std::min(stage_chunks(k * S), static_cast<int>(std::min<size_t>(kBatchChunks, S / 4096))));
     const hipStream_t s = L.stream;
     L.begin(s);
-    rsmi::MatArgs a = base_args(c, din, 0, dout, 0, span, S, 1);
-    set_patterns(c, 1, c->d_encpat.p, a);
-    a.stripe_desc = nullptr;
-    hipError_t e = launch_encode(c, a, s);
-    L.end(s);
-    if (e == hipSuccess) e = rsmi::wait_event(L.dev_done);
-    if (e == hipSuccess) {
-        const uint8_t* out = static_cast<const uint8_t*>(L.st_out.p);
-        if (span == S) {
-            std::memcpy(parity, out, m * S);
-        } else {
-            for (size_t t = 0; t < m; ++t) std::memcpy(parity + t * S, out + t * span, S);
-        }
+    hipError_t e = hipSuccess;
+    int launched = 0;
+    for (int ch = 0; ch < nch && e == hipSuccess; ++ch) {
+        // chunk ch's columns of every data shard into staging, then its launch
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        for (size_t j = 0; j < k; ++j) std::memcpy(st + j * span + off, input + j * S + off, w);
+        rsmi::MatArgs a = base_args(c, static_cast<uint8_t*>(din) + off, 0, static_cast<uint8_t*>(dout) + off, 0, span, w, 1);
+        set_patterns(c, 1, c->d_encpat.p, a);
+        a.stripe_desc = nullptr;
+        e = launch_encode(c, a, s);
+        if (e == hipSuccess) e = hipEventRecord(L.ev[ch], s);
+        if (e == hipSuccess) ++launched;
     }
+    L.end(s);
+    for (int ch = 0; ch < launched; ++ch) {
+        const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
+        if (e == hipSuccess) e = w8;
+        if (e != hipSuccess) continue;
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        for (size_t t = 0; t < m; ++t) std::memcpy(parity + t * S + off, out + t * span + off, w);
+    }
+    if (launched < nch) (void)rsmi::wait_event(L.dev_done);
     *rc = e == hipSuccess ? RS_OK : RS_EDEVICE;
     return true;
 }
