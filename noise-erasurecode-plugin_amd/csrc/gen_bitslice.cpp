@@ -93,13 +93,6 @@ bool kInputBarrier = false;
 // wave-uniform branch per (syndrome, output) instead of coded as padding;
 // the syndrome's bit fields are extracted once per group for all outputs.
 bool kSolveTail = false;
-// Solve in syndrome pairs (-C): when both rows t, t+1 are survivors, an
-// output word takes the six table lookups through three XOR3s (instead of two
-// per syndrome).
-bool kSolvePairs = false;
-// With -C, -D: a group of fewer than R outputs (the last group when e is not
-// a multiple of R) runs a body coded for exactly its outputs (no padding).
-bool kSolveDispatch = false;
 constexpr int kTopMinM = 12;
 
 void emit_common(FILE* f) {
@@ -355,105 +348,6 @@ void emit_kernel(FILE* f, int k, int n) {
 // erasures use only top rows; the host routes a stripe here when every
 // parity row its pattern uses (syndromes and erased-parity outputs) is one
 // of them.  Fewer accumulators -> fewer VGPRs -> more waves per SIMD.
-// The solve of -C: the output group loop (left open: the caller closes it),
-// syndrome rows T0..m-1 taken in pairs with literal accumulator indices.  A
-// pair whose rows are both survivors codes each output word as
-// xor3(xor3(xor3(out, a0, a1), a2, b0), b1, b2) over its six lookups; a lone
-// survivor row as gf_mac.  Outputs past e in the last group are coded as
-// padding (zero tables), as in the default solve.
-void emit_solve_pairs(FILE* f, int m, int T0) {
-    std::fprintf(f, "%s", R"(#pragma unroll 1
-    for (uint32_t g = 0; g < e; g += R) {
-)");
-    auto group = [&]() {
-    std::fprintf(f, "%s", R"(        uint32_t oid[RG];
-#pragma unroll
-        for (int r = 0; r < RG; ++r)
-            oid[r] = g + r < e ? static_cast<uint32_t>(__builtin_amdgcn_readlane(did_l, g + r)) : 0xFFFFFFFFu;
-        uint32_t out[RG][8];
-#pragma unroll
-        for (int r = 0; r < RG; ++r)
-#pragma unroll
-            for (int w = 0; w < 8; ++w) out[r][w] = 0u;
-)");
-    auto enter = [&](int t) {
-        const int a = 8 * (t - T0);
-        std::fprintf(f, "            asm volatile(\"\" : \"+v\"(acc[%d]), \"+v\"(acc[%d]), \"+v\"(acc[%d]), \"+v\"(acc[%d]), "
-                        "\"+v\"(acc[%d]), \"+v\"(acc[%d]), \"+v\"(acc[%d]), \"+v\"(acc[%d]));\n",
-                     a, a + 1, a + 2, a + 3, a + 4, a + 5, a + 6, a + 7);
-    };
-    auto tables = [&](const char* T, int t) {
-        std::fprintf(f, "            uint32_t %s[RG][5];\n#pragma unroll\n            for (int r = 0; r < RG; ++r)\n#pragma unroll\n"
-                        "                for (int i = 0; i < 5; ++i) %s[r][i] = mtab[g + r][%d][i];\n",
-                     T, T, t - T0);
-    };
-    auto single = [&](int t) {
-        enter(t);
-        tables("TA", t);
-        std::fprintf(f, "#pragma unroll\n            for (int w = 0; w < 8; ++w) {\n"
-                        "                const gfd::Fields fa = gfd::fields(acc[%d + w]);\n#pragma unroll\n"
-                        "                for (int r = 0; r < RG; ++r) out[r][w] = gfd::gf_mac(out[r][w], TA[r], fa.a, fa.b, fa.c);\n"
-                        "            }\n",
-                     8 * (t - T0));
-    };
-    for (int t = T0; t < m; t += 2) {
-        std::fprintf(f, "        // syndrome rows %d%s\n", t, t + 1 < m ? (" and " + std::to_string(t + 1)).c_str() : "");
-        if (t + 1 < m) {
-            std::fprintf(f, "        if (((pmask >> %d) & 3u) == 3u) {\n", t);
-            enter(t);
-            enter(t + 1);
-            tables("TA", t);
-            tables("TB", t + 1);
-            std::fprintf(f, "#pragma unroll\n            for (int w = 0; w < 8; ++w) {\n"
-                            "                const gfd::Fields fa = gfd::fields(acc[%d + w]), fb = gfd::fields(acc[%d + w]);\n"
-                            "#pragma unroll\n"
-                            "                for (int r = 0; r < RG; ++r) out[r][w] = gfd::gf_mac2(out[r][w], TA[r], fa, TB[r], fb);\n"
-                            "            }\n        } else if ((pmask >> %d) & 1u) {\n",
-                         8 * (t - T0), 8 * (t + 1 - T0), t);
-            single(t);
-            std::fprintf(f, "        } else if ((pmask >> %d) & 1u) {\n", t + 1);
-            single(t + 1);
-            std::fprintf(f, "        }\n");
-        } else {
-            std::fprintf(f, "        if ((pmask >> %d) & 1u) {\n", t);
-            single(t);
-            std::fprintf(f, "        }\n");
-        }
-        // erased parity outputs take their own q rows
-        for (int u = t; u < std::min(t + 2, m); ++u)
-            std::fprintf(f, "        if ((qmask >> %d) & 1u) {\n#pragma unroll\n            for (int r = 0; r < RG; ++r)\n"
-                            "                if (oid[r] == static_cast<uint32_t>(K + %d)) {\n#pragma unroll\n"
-                            "                    for (int w = 0; w < 8; ++w) out[r][w] ^= acc[%d + w];\n                }\n        }\n",
-                         u, u, 8 * (u - T0));
-        std::fprintf(f, "#pragma unroll\n        for (int r = 0; r < RG; ++r)\n"
-                        "            asm volatile(\"\" : \"+v\"(out[r][0]), \"+v\"(out[r][1]), \"+v\"(out[r][2]), \"+v\"(out[r][3]),\n"
-                        "                              \"+v\"(out[r][4]), \"+v\"(out[r][5]), \"+v\"(out[r][6]), \"+v\"(out[r][7])::\"memory\");\n");
-    }
-    std::fprintf(f, "%s", R"(#pragma unroll
-        for (int r = 0; r < RG; ++r) {
-            if (g + r >= e) break;
-            uint8_t* o = shard(oid[r]);
-            if (oka) bs_store(o, offa, out[r][0], out[r][1], out[r][2], out[r][3]);
-            if (okb) bs_store(o, offb, out[r][4], out[r][5], out[r][6], out[r][7]);
-        }
-)");
-    };
-    if (!kSolveDispatch) {
-        std::fprintf(f, "        {\n        constexpr int RG = R;\n");
-        group();
-        std::fprintf(f, "        }\n");
-        return;
-    }
-    // The group's output count picks a body coded for exactly that many
-    // outputs: the last group of e outputs carries no padding.
-    std::fprintf(f, "        const uint32_t nr = min(e - g, static_cast<uint32_t>(R));\n");
-    for (int rr = kRecRows; rr >= 1; --rr) {
-        std::fprintf(f, "        %sif (nr == %du) {\n        constexpr int RG = %d;\n", rr == kRecRows ? "" : "else ", rr, rr);
-        group();
-        std::fprintf(f, "        }\n");
-    }
-}
-
 std::string rec_name(int k, int m, int top) {
     return "rs_bitslice_rec_k" + std::to_string(k) + "_m" + std::to_string(m) +
            (top < m ? "_t" + std::to_string(top) : std::string());
@@ -692,9 +586,6 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
             for (int i = 0; i < 8; ++i) acc[8 * (t - T0) + i] = w[i];
         }
 )");
-    if (kSolvePairs)
-        emit_solve_pairs(f, m, T0);
-    else
     std::fprintf(f, "#pragma unroll 1\n    for (uint32_t g = 0; g < e; g += R) {\n%s",
                  kSolveTail ? R"SOLVE(        uint32_t oid[R];
 #pragma unroll
@@ -910,16 +801,6 @@ int main(int argc, char** argv) {
         argv += 1;
         argc -= 1;
     }
-    if (argc >= 2 && std::string(argv[1]) == "-C") {
-        kSolvePairs = true;
-        argv += 1;
-        argc -= 1;
-    }
-    if (argc >= 2 && std::string(argv[1]) == "-D") {
-        kSolveDispatch = true;
-        argv += 1;
-        argc -= 1;
-    }
     if (argc >= 2 && std::string(argv[1]) == "-u") {
         kTopGuard = true;
         argv += 1;
@@ -959,7 +840,7 @@ int main(int argc, char** argv) {
         argc -= 2;
     }
     if (argc < 3) {
-        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N|-Y] [-L] [-C] [-D] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N|-Y] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
         return 2;
     }
     std::vector<std::pair<int, int>> codes;

@@ -64,18 +64,5 @@ __device__ __forceinline__ uint32_t gf_mac(uint32_t acc, const uint32_t* T, uint
     return xor3(acc, la, lb) ^ lc;
 }
 
-// acc ^= c * x ^ d * y: six lookups through three XOR3s (two gf_mac calls
-// take four XOR ops).
-__device__ __forceinline__ uint32_t gf_mac2(uint32_t acc, const uint32_t* A, const Fields& x, const uint32_t* B,
-                                            const Fields& y) {
-    const uint32_t a0 = __builtin_amdgcn_perm(A[1], A[0], x.a);
-    const uint32_t a1 = __builtin_amdgcn_perm(A[3], A[2], x.b);
-    const uint32_t a2 = __builtin_amdgcn_perm(A[4], A[4], x.c);
-    const uint32_t b0 = __builtin_amdgcn_perm(B[1], B[0], y.a);
-    const uint32_t b1 = __builtin_amdgcn_perm(B[3], B[2], y.b);
-    const uint32_t b2 = __builtin_amdgcn_perm(B[4], B[4], y.c);
-    return xor3(xor3(xor3(acc, a0, a1), a2, b0), b1, b2);
-}
-
 }  // namespace gfd
 }  // namespace rsmi
