@@ -1033,16 +1033,18 @@ def test_xcd_block_order_matches_natural(k, n, S, stripes):
         f.close()
 
 
-@pytest.mark.parametrize("S", [209_700, 209_716, 209_733, 2 * 1024 * 1024 + 5])
+@pytest.mark.parametrize("S", [1, 17, 8_200, 65_539, 209_700, 209_716, 209_733, 2 * 1024 * 1024 + 5])
 @pytest.mark.parametrize("stage_small", [True, False])
 def test_host_api_staging_threshold(S, stage_small, monkeypatch):
     """rs_encode / rs_decode on pageable buffers around the one-shot staging
     threshold (k x round_up(S, 16) <= 2 MiB: staged once and coded by one
     launch, rsmi.cpp encode_staged / decode_staged) and past it (the chunked
     pipeline, several 8 MiB chunks at S = 2 MiB + 5), unaligned shard
-    lengths included; RSMI_NO_STAGE_SMALL forces the pipeline for the small
-    sizes too.  Bit-exact vs the oracle; decode with 4 drops including
-    parity."""
+    lengths included, from one byte (one chunk below 8 KiB per shard, two
+    column chunks from 256 KiB a message); RSMI_NO_STAGE_SMALL forces the
+    pipeline for the small sizes too.  Bit-exact vs the oracle; decode with 4
+    drops including parity, and with only parity lost (no launch: the
+    present shares are copied)."""
     import ctypes
     if not stage_small:
         monkeypatch.setenv("RSMI_NO_STAGE_SMALL", "1")
@@ -1057,7 +1059,7 @@ def test_host_api_staging_threshold(S, stage_small, monkeypatch):
     assert lib.rs_encode(f.handle, P(data.ctypes.data), k * S, P(par.ctypes.data)) == 0
     assert par.tobytes() == oracle.encode(E, k, n, data.tobytes())
     shard = lambda i: data[i * S:(i + 1) * S] if i < k else par[(i - k) * S:(i - k + 1) * S]
-    for lost in ((0, 3, 7, 12), (1, 2, 10, 11), (9, 10, 11, 13)):
+    for lost in ((0, 3, 7, 12), (1, 2, 10, 11), (9, 10, 11, 13), (10, 11, 12, 13)):
         keep = [i for i in range(n) if i not in lost]
         bufs = [np.ascontiguousarray(shard(i)) for i in keep]
         dst = np.zeros(k * S, dtype=np.uint8)
@@ -1065,3 +1067,49 @@ def test_host_api_staging_threshold(S, stage_small, monkeypatch):
         ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs[::-1]])
         assert lib.rs_decode(f.handle, nums, ptrs, k, S, P(dst.ctypes.data)) == 0
         assert np.array_equal(dst, data), lost
+
+
+_CHUNKS_CHILD = r"""
+import ctypes, os, sys
+import numpy as np
+sys.path[:0] = [os.environ["ROOT"], os.path.join(os.environ["ROOT"], "noise-erasurecode-plugin_amd")]
+import rsmi
+from oracle import oracle
+k, n = 10, 14
+m = n - k
+f = rsmi.NewFEC(k, n)
+lib = rsmi.load()
+E = oracle.fec_matrix(k, n)
+P = ctypes.c_void_p
+for S in (8_193, 30_001, 104_858, 209_700):
+    data = oracle.splitmix_bytes(k * S, S)
+    par = np.zeros(m * S, dtype=np.uint8)
+    assert lib.rs_encode(f.handle, P(data.ctypes.data), k * S, P(par.ctypes.data)) == 0
+    assert par.tobytes() == oracle.encode(E, k, n, data.tobytes()), S
+    shard = lambda i: data[i * S:(i + 1) * S] if i < k else par[(i - k) * S:(i - k + 1) * S]
+    for lost in ((0, 3, 7, 12), (9, 10, 11, 13)):
+        keep = [i for i in range(n) if i not in lost]
+        bufs = [np.ascontiguousarray(shard(i)) for i in keep]
+        dst = np.zeros(k * S, dtype=np.uint8)
+        nums = (ctypes.c_int * k)(*keep)
+        ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
+        assert lib.rs_decode(f.handle, nums, ptrs, k, S, P(dst.ctypes.data)) == 0
+        assert np.array_equal(dst, data), (S, lost)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("chunks", ["1", "3", "4"])
+def test_host_api_forced_stage_chunks(chunks):
+    """Staged small messages coded in 1, 3 or 4 column chunks
+    (RSMI_STAGE_CHUNKS, read once per process: a child process each; the
+    default 2 is covered above): each chunk is staged, launched and copied out
+    on its own, chunk offsets 16-byte aligned, the last chunk ragged.
+    Bit-exact vs the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RSMI_STAGE_CHUNKS=chunks, ROOT=root)
+    p = subprocess.run([sys.executable, "-c", _CHUNKS_CHILD], env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120)
+    assert p.returncode == 0 and p.stdout.strip() == "ok", p.stderr[-3000:]
