@@ -424,7 +424,8 @@ def config1_leg(local, reps=50):
     f = rsmi.FEC(k, n, device=local)
     P = ctypes.c_void_p
     parity = np.zeros(m * S, dtype=np.uint8)
-    enc_ms = _median_ms(lambda: lib.rs_encode(f.handle, P(blob_np.ctypes.data), L, P(parity.ctypes.data)), reps)
+    bptr, pptr = P(blob_np.ctypes.data), P(parity.ctypes.data)
+    enc_ms = _median_ms(lambda: lib.rs_encode(f.handle, bptr, L, pptr), reps)
     E = oracle.fec_matrix(k, n)
     ref_par = np.frombuffer(oracle.encode(E, k, n, blob_np.tobytes()), dtype=np.uint8)
     if not np.array_equal(parity, ref_par):
@@ -436,10 +437,16 @@ def config1_leg(local, reps=50):
     bufs = [np.ascontiguousarray(shard(i)) for i in keep]
     dst = np.zeros(L, dtype=np.uint8)
 
+    # The share arrays are built once, as a cgo caller holds them: keep is in
+    # ascending order, so rs_decode's in-place sort (sort.Sort(byNumber))
+    # leaves them as they are, and no call pays for the binding's array
+    # construction (~1 us per numpy .ctypes access).
+    nums = (ctypes.c_int * k)(*keep)
+    ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
+    dptr = P(dst.ctypes.data)
+
     def dec():
-        nums = (ctypes.c_int * k)(*keep)
-        ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
-        rc = lib.rs_decode(f.handle, nums, ptrs, k, S, P(dst.ctypes.data))
+        rc = lib.rs_decode(f.handle, nums, ptrs, k, S, dptr)
         if rc:
             raise RuntimeError(f"config1: rs_decode returned {rc}")
     dec_ms = _median_ms(dec, reps)
@@ -453,10 +460,12 @@ def config1_leg(local, reps=50):
     dst_a = np.zeros(L, dtype=np.uint8)
     in0 = f.stat(f.STAT_DECODES_IN_PLACE)
 
+    anums = (ctypes.c_int * k)(*keep)
+    aptrs_c = (ctypes.c_void_p * k)(*aptrs)
+    daptr = P(dst_a.ctypes.data)
+
     def dec_arena():
-        nums = (ctypes.c_int * k)(*keep)
-        ptrs = (ctypes.c_void_p * k)(*aptrs)
-        rc = lib.rs_decode(f.handle, nums, ptrs, k, S, P(dst_a.ctypes.data))
+        rc = lib.rs_decode(f.handle, anums, aptrs_c, k, S, daptr)
         if rc:
             raise RuntimeError(f"config1: rs_decode (arena) returned {rc}")
     dec_arena_ms = _median_ms(dec_arena, reps)
@@ -499,14 +508,21 @@ def config1_leg(local, reps=50):
     par = np.zeros(m * S, dtype=np.uint8)
     dst_cpu = np.zeros(L, dtype=np.uint8)
     present = [i for i in range(k) if i not in lost]
+    # The oracle's C entry points with their pointers bound once, like the
+    # GPU calls above (no per-call numpy .ctypes accesses on either side).
+    olib = oracle.lib()
+    Ec = np.ascontiguousarray(E)
+    e_p, b_p, par_p, dst_p, er_p = (P(a_.ctypes.data) for a_ in (Ec, blob_np, par, dst_cpu, er))
+    src0, dst0 = blob_np.ctypes.data, dst_cpu.ctypes.data
     for name, simd in (("scalar_1t", False), ("avx2_1t", True)):
-        e_ms = _median_ms(lambda: oracle.encode_batch(E, k, n, blob_np, S, 1, simd=simd, threads=1, out=par),
-                          max(5, reps // 5))
+        e_ms = _median_ms(lambda: olib.orc_encode_batch(e_p, k, n, b_p, par_p, S, 1, int(simd), 1), max(5, reps // 5))
+        if not np.array_equal(par, ref_par):
+            raise RuntimeError("config1: the oracle's encode differs")
 
         def cpu_dec():
             for i in present:
-                dst_cpu[i * S:(i + 1) * S] = blob_np[i * S:(i + 1) * S]
-            return oracle.reconstruct_batch(E, k, n, dst_cpu, par, S, 1, er, simd=simd, threads=1)
+                ctypes.memmove(dst0 + i * S, src0 + i * S, S)
+            return olib.orc_reconstruct_batch(e_p, k, n, dst_p, par_p, S, 1, er_p, int(simd), 1)
         d_ms = _median_ms(cpu_dec, max(5, reps // 5))
         if not np.array_equal(dst_cpu, blob_np):
             raise RuntimeError("config1: the oracle's decode did not return the blob")

@@ -125,8 +125,10 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);
     const uint64_t sv = b / a.chunks;
     // Stripe descriptor = {stripe, pattern id << 8 | outputs} (one dependent
-    // load); encode (no table) is stripe sv, pattern 0, all m parity rows.
-    uint2 desc = make_uint2(static_cast<uint32_t>(sv), a.m);
+    // load); without a table it is stripe sv with a.desc0 (encode: pattern 0,
+    // all m parity rows) -- a single-message decode then starts its pattern
+    // and survivor reads without a dependent read of host memory first.
+    uint2 desc = make_uint2(static_cast<uint32_t>(sv), a.desc0 ? a.desc0 : a.m);
     if (a.stripe_desc) desc = a.stripe_desc[sv];
     const uint64_t s = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(desc.x));
     const uint32_t sw = __builtin_amdgcn_readfirstlane(desc.y);
@@ -151,14 +153,17 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
         return id < a.k ? a.data + s * a.data_ss + static_cast<uint64_t>(id) * a.pitch
                         : a.parity + s * a.parity_ss + static_cast<uint64_t>(id - a.k) * a.pitch;
     };
-    const uint32_t* srcid = a.src + static_cast<size_t>(pat) * k;
+    // a.src == nullptr: survivor j is shard id j (no id read before the
+    // survivor loads).
+    const uint32_t* srcid = a.src ? a.src + static_cast<size_t>(pat) * k : nullptr;
     const uint32_t* dstid = a.dst + static_cast<size_t>(pat) * a.dst_stride + row0;
     uint8_t* sp[kRegPtrs ? K : 1];
     if constexpr (kRegPtrs) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) sp[j] = uniform_ptr(shard(__builtin_amdgcn_readfirstlane(srcid[j])));
+        for (int j = 0; j < K; ++j)
+            sp[j] = uniform_ptr(shard(srcid ? __builtin_amdgcn_readfirstlane(srcid[j]) : static_cast<uint32_t>(j)));
     } else {
-        for (int i = threadIdx.x; i < k; i += BT) sptr[i] = shard(srcid[i]);
+        for (int i = threadIdx.x; i < k; i += BT) sptr[i] = shard(srcid ? srcid[i] : static_cast<uint32_t>(i));
     }
     const uint32_t last = a.ncols16 - 1;
     // Survivor loads of the block's first iteration are issued before the

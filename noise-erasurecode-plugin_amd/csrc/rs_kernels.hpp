@@ -30,7 +30,9 @@ struct MatArgs {
     uint32_t iters;      // block iterations per chunk
     uint32_t k, m;
     const uint8_t* coef;         // [npat][m][k]
-    const uint32_t* src;         // [npat][k]   survivor shard ids
+    const uint32_t* src;         // [npat][k]   survivor shard ids, or nullptr: survivor j is
+                                 // shard id j (single-pattern launches whose shard table or
+                                 // strided layout is already in survivor order)
     const uint32_t* dst;         // [npat][dst_stride] output shard ids (padded, >= 16)
     uint32_t dst_stride;
     const uint2* stripe_desc;    // [stripes] {stripe index, pattern id << 8 | outputs}
@@ -40,6 +42,8 @@ struct MatArgs {
                                  // mode: data/parity/strides/pitch unused), or nullptr
     uint32_t xcd;                // XCD-aware block order (xcd.hpp): blocks per region, or 0
                                  // (natural); ~0u = all of a stripe's blocks (set at launch)
+    uint32_t desc0;              // stripe_desc == nullptr: every stripe's {pattern << 8 |
+                                 // outputs} word (0: pattern 0 with all m rows, the encode)
 };
 
 // Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel

@@ -149,6 +149,7 @@ struct GrowBuf {
 // x2, so the retired buffers never exceed the live one.
 struct Staging {
     void* p = nullptr;
+    void* dev = nullptr;  // p's device alias (queried once per allocation, not per call)
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
@@ -165,6 +166,7 @@ struct Staging {
         if (hipHostMalloc(&np, want, hipHostMallocDefault) != hipSuccess) return false;
         if (p) retired.push_back(p);
         p = np;
+        if (hipHostGetDevicePointer(&dev, np, 0) != hipSuccess) dev = np;
         cap = want;
         return true;
     }
@@ -178,6 +180,7 @@ struct Staging {
         if (p) (void)hipHostFree(p);
         if (done) (void)hipEventDestroy(done);
         p = nullptr;
+        dev = nullptr;
         done = nullptr;
     }
 };
@@ -956,9 +959,7 @@ int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vecto
             if (!L.st_onepat.acquire(pbytes)) return RS_ENOMEM;
             pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(),
                           static_cast<uint8_t*>(L.st_onepat.p));
-            void* alias = nullptr;
-            if (hipHostGetDevicePointer(&alias, L.st_onepat.p, 0) != hipSuccess) alias = L.st_onepat.p;
-            pat = alias;
+            pat = L.st_onepat.dev;
         } else {
             std::vector<uint8_t> hp(pbytes);
             pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), hp.data());
@@ -1076,8 +1077,7 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     const size_t span = round_up(S, 16);
     if (S == 0 || static_cast<size_t>(k) * span > kStageSmall || std::getenv("RSMI_NO_STAGE_SMALL")) return false;
     if (!L.st_in.acquire(static_cast<size_t>(k) * span)) return false;
-    void* alias = nullptr;
-    if (hipHostGetDevicePointer(&alias, L.st_in.p, 0) != hipSuccess) alias = L.st_in.p;
+    void* alias = L.st_in.dev;
     std::vector<int> surv = rsmi::choose_survivors(present.data(), k, c->n);
     std::vector<uint64_t> dev(k);
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
@@ -1128,15 +1128,17 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
     for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
     pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), host);
-    void* halias = nullptr;
-    if (hipHostGetDevicePointer(&halias, host, 0) != hipSuccess) halias = host;
+    void* halias = L.st_onepat.dev;
     uint64_t oalias = 0;
-    if (!dst_direct) {
-        void* oa = nullptr;
-        if (hipHostGetDevicePointer(&oa, L.st_out.p, 0) != hipSuccess) oa = L.st_out.p;
-        oalias = reinterpret_cast<uint64_t>(oa);
-    }
+    if (!dst_direct) oalias = reinterpret_cast<uint64_t>(L.st_out.dev);
     const void* pat = halias;
+    // Survivors at a common pitch (decode_staged's staging) with outputs in
+    // the output staging: the strided layout, no shard table.  The kernel's
+    // first reads -- the pattern's coefficients and the survivors -- then go
+    // out together (no descriptor, survivor-id or shard-table read before
+    // them, each a PCIe round trip).
+    bool strided = !dst_direct;
+    for (int jj = 1; jj < k && strided; ++jj) strided = dev[jj] == dev[0] + static_cast<uint64_t>(jj) * span;
     const hipStream_t s = L.stream;
     L.begin(s);
     hipError_t err = hipSuccess;
@@ -1144,15 +1146,20 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     for (int ch = 0; ch < nch && err == hipSuccess; ++ch) {
         const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
         if (stage) stage(off, w);
-        uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff + ch * n8);
-        for (int jj = 0; jj < k; ++jj) tab[jj] = dev[jj] + off;
-        for (int t = 0; t < e; ++t)
-            tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span) + off
-                                    : oalias + static_cast<uint64_t>(t) * span + off;
-        rsmi::MatArgs a = base_args(c, nullptr, 0, nullptr, 0, span, w, 1);
+        rsmi::MatArgs a = strided ? base_args(c, reinterpret_cast<void*>(dev[0] + off), 0,
+                                              reinterpret_cast<void*>(oalias + off), 0, span, w, 1)
+                                  : base_args(c, nullptr, 0, nullptr, 0, span, w, 1);
         set_patterns(c, 1, pat, a);
-        a.stripe_desc = first_stripe_desc(c, pat);
-        a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
+        a.src = nullptr;                    // survivor j is id j, output t is id k + t
+        a.desc0 = static_cast<uint32_t>(e);  // pattern 0, e outputs
+        if (!strided) {
+            uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff + ch * n8);
+            for (int jj = 0; jj < k; ++jj) tab[jj] = dev[jj] + off;
+            for (int t = 0; t < e; ++t)
+                tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span) + off
+                                        : oalias + static_cast<uint64_t>(t) * span + off;
+            a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
+        }
         err = rsmi::launch_matmul(a, e, s);
         if (err == hipSuccess) err = hipEventRecord(L.ev[ch], s);
         if (err == hipSuccess) ++launched;
@@ -1180,9 +1187,7 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
     const size_t k = c->k, m = c->m, span = round_up(S, 16);
     if (S == 0 || k * span > kStageSmall || std::getenv("RSMI_NO_STAGE_SMALL")) return false;
     if (!L.st_in.acquire(k * span) || !L.st_out.acquire(m * span)) return false;
-    void *din = nullptr, *dout = nullptr;
-    if (hipHostGetDevicePointer(&din, L.st_in.p, 0) != hipSuccess) din = L.st_in.p;
-    if (hipHostGetDevicePointer(&dout, L.st_out.p, 0) != hipSuccess) dout = L.st_out.p;
+    void *din = L.st_in.dev, *dout = L.st_out.dev;
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
     const uint8_t* out = static_cast<const uint8_t*>(L.st_out.p);
     const int nch = std::max(1, std::min(stage_chunks(k * S), static_cast<int>(std::min<size_t>(kBatchChunks, S / 4096))));
