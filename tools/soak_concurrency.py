@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Concurrency soak of one RS(64,16) context (SURVEY §8b threading): for
+"""Concurrency soak of one context (RS(64,16) by default; --code 10:14
+--shard 104858 gives config-1-sized messages, whose host-API calls take the
+two-chunk staged path) (SURVEY §8b threading): for
 --seconds, T threads mix every C-ABI entry point that shares the context's
 pattern cache -- rs_decode (host API), rs_decode_batch, rs_encode and
 rs_reconstruct_stripes on their own device stripes with fresh erasure
@@ -8,7 +10,7 @@ evicted over and over while other threads read it.  Every result is checked
 (host API against the input, device stripes against a clone).  Prints one
 JSON line with call counts, evictions and failures.
 
-    RSMI_PATTERN_CAP=2000 python tools/soak_concurrency.py [--seconds 60 --threads 8]
+    RSMI_PATTERN_CAP=2000 python tools/soak_concurrency.py [--seconds 60 --threads 8 --code K:N --shard S]
 """
 import argparse
 import ctypes
@@ -29,12 +31,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--code", default="64:80")
+    ap.add_argument("--shard", type=int, default=4096, help="shard bytes of thread 0 (thread t: + 16 t)")
     a = ap.parse_args()
     import rsmi
     from oracle import oracle
 
     lib = rsmi.load()
-    k, n, m = 64, 80, 16
+    k, n = (int(v) for v in a.code.split(":"))
+    m = n - k
     f = rsmi.FEC(k, n)
     P = ctypes.c_void_p
     stop = time.time() + a.seconds
@@ -43,18 +48,26 @@ def main():
     lock = threading.Lock()
 
     def worker(tid):
+        try:
+            body(tid)
+        except Exception as e:  # a thread that dies outside the checked loop is a failure too
+            with lock:
+                failures.append(f"thread {tid}: {e!r}")
+
+    def body(tid):
         rng = np.random.default_rng(1000 + tid)
-        S = 4096 + 16 * tid
+        S = a.shard + 16 * tid
         blob = oracle.splitmix_bytes(k * S, tid)
         par = np.zeros(m * S, dtype=np.uint8)
         assert lib.rs_encode(f.handle, P(blob.ctypes.data), k * S, P(par.ctypes.data)) == 0
         shard = lambda i: blob[i * S:(i + 1) * S] if i < k else par[(i - k) * S:(i - k + 1) * S]
         stripes = 64
+        Sd = (S + 15) // 16 * 16  # device stripes: 16-byte pitch (rs_encode_stripes)
         stream = torch.cuda.Stream()
-        data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
-        parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+        data = torch.empty(stripes * k * Sd, dtype=torch.uint8, device="cuda")
+        parity = torch.empty(stripes * m * Sd, dtype=torch.uint8, device="cuda")
         f.fill_splitmix(data.data_ptr(), data.numel(), 77 + tid, stream.cuda_stream)
-        f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, stream.cuda_stream)
+        f.encode_stripes(data.data_ptr(), k * Sd, parity.data_ptr(), m * Sd, Sd, Sd, stripes, stream.cuda_stream)
         stream.synchronize()
         d0, p0 = data.clone(), parity.clone()
         local = dict.fromkeys(counts, 0)
@@ -97,9 +110,9 @@ def main():
                         er[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 1
                     with torch.cuda.stream(stream):
                         mask = torch.from_numpy(er).to("cuda", non_blocking=False).bool()
-                        data.view(stripes, k, S)[mask[:, :k]] = 0
-                        parity.view(stripes, m, S)[mask[:, k:]] = 0
-                    f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes,
+                        data.view(stripes, k, Sd)[mask[:, :k]] = 0
+                        parity.view(stripes, m, Sd)[mask[:, k:]] = 0
+                    f.reconstruct_stripes(data.data_ptr(), k * Sd, parity.data_ptr(), m * Sd, Sd, Sd, stripes,
                                           er.tobytes(), stream.cuda_stream)
                     stream.synchronize()
                     assert torch.equal(data, d0) and torch.equal(parity, p0)
@@ -118,7 +131,7 @@ def main():
         t.start()
     for t in threads:
         t.join()
-    print(json.dumps({"seconds": a.seconds, "threads": a.threads, "calls": counts,
+    print(json.dumps({"code": a.code, "shard": a.shard, "seconds": a.seconds, "threads": a.threads, "calls": counts,
                       "pattern_cap": os.environ.get("RSMI_PATTERN_CAP"), "evictions": f.pattern_evictions(),
                       "patterns": f.pattern_count(), "leases": f.stat(f.STAT_LEASES),
                       "failures": len(failures), "first_failures": failures[:5]}))
