@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Randomised soak of the host-buffer C ABI (rs_encode / rs_decode, the cgo
+calls replacing infectious Encode / Decode at main.go:262 / :77) against the
+oracle: random (k, n), shard lengths from 1 byte to past the one-shot staging
+threshold (aligned and ragged), k to n shares in random order, sometimes with
+one corrupted share (Correct / Berlekamp-Welch), survivors in pageable
+memory, in an engine-pinned rs_arena (read in place) or mixed, dst pageable
+or engine-pinned.  Every parity and every decoded message is compared with
+the oracle's.  Prints one JSON line.
+
+usage: tools/fuzz_host_api.py [--seconds 120 | --cases N] [--seed 1]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "noise-erasurecode-plugin_amd")]
+
+import numpy as np  # noqa: E402
+
+CODES = [(10, 14), (64, 80), (8, 14), (4, 6), (17, 49), (1, 3), (32, 40), (100, 120), (200, 256), (2, 4)]
+
+
+def run(seconds=None, cases=None, seed=1):
+    import rsmi
+    from oracle import oracle
+
+    rng = np.random.default_rng(seed)
+    lib = rsmi.load()
+    P = ctypes.c_void_p
+    fecs, mats = {}, {}
+    stats = {"cases": 0, "encode": 0, "decode_k": 0, "decode_more": 0, "corrupted": 0, "arena": 0,
+             "pinned_dst": 0, "failures": 0}
+    first = []
+    t0 = time.time()
+    while (cases is None or stats["cases"] < cases) and (seconds is None or time.time() - t0 < seconds):
+        k, n = CODES[int(rng.integers(0, len(CODES)))]
+        m = n - k
+        if (k, n) not in fecs:
+            fecs[(k, n)] = rsmi.FEC(k, n)
+            mats[(k, n)] = oracle.fec_matrix(k, n)
+        f, E = fecs[(k, n)], mats[(k, n)]
+        smax = max(1, min(300_000, 4_000_000 // k))
+        S = int(np.exp(rng.uniform(0, np.log(smax))))
+        if rng.random() < 0.3:
+            S = max(16, S // 16 * 16)
+        data = oracle.splitmix_bytes(k * S, int(rng.integers(0, 2**32)))
+        par = np.zeros(m * S, dtype=np.uint8)
+        case = f"k={k} n={n} S={S}"
+        stats["cases"] += 1
+        try:
+            assert lib.rs_encode(f.handle, P(data.ctypes.data), k * S, P(par.ctypes.data)) == 0, case + " encode rc"
+            assert par.tobytes() == oracle.encode(E, k, n, data.tobytes()), case + " parity"
+            stats["encode"] += 1
+            shard = lambda i: data[i * S:(i + 1) * S] if i < k else par[(i - k) * S:(i - k + 1) * S]
+            cnt = k if rng.random() < 0.6 else int(rng.integers(k, n + 1))
+            ids = [int(v) for v in rng.choice(n, size=cnt, replace=False)]
+            bufs = {i: np.ascontiguousarray(shard(i)).copy() for i in ids}
+            corrupt = cnt >= k + 2 and rng.random() < 0.5
+            if corrupt:
+                v = ids[int(rng.integers(0, cnt))]
+                pos = int(rng.integers(0, S))
+                bufs[v][pos] ^= np.uint8(1 + int(rng.integers(0, 255)))
+                stats["corrupted"] += 1
+            where = rng.random()
+            arena = None
+            ptr = {}
+            if where < 0.35:  # every survivor in an engine-pinned arena slot
+                arena = rsmi.Arena(sum(S + 256 for _ in ids) + 4096)
+                for i in ids:
+                    ptr[i] = arena.put(bufs[i].tobytes())
+                stats["arena"] += 1
+            elif where < 0.5 and cnt > 1:  # mixed: some pinned, some pageable
+                arena = rsmi.Arena(sum(S + 256 for _ in ids) + 4096)
+                for j, i in enumerate(ids):
+                    ptr[i] = arena.put(bufs[i].tobytes()) if j % 2 else bufs[i].ctypes.data
+            else:
+                for i in ids:
+                    ptr[i] = bufs[i].ctypes.data
+            pinned_dst = rng.random() < 0.25
+            if pinned_dst:
+                dp = lib.rs_pinned_alloc(max(k * S, 16))
+                ctypes.memset(dp, 0, max(k * S, 16))
+                stats["pinned_dst"] += 1
+            else:
+                dst = np.zeros(k * S, dtype=np.uint8)
+                dp = dst.ctypes.data
+            nums = (ctypes.c_int * cnt)(*ids)
+            ptrs = (ctypes.c_void_p * cnt)(*[ptr[i] for i in ids])
+            rc = lib.rs_decode(f.handle, nums, ptrs, cnt, S, P(dp))
+            got = ctypes.string_at(dp, k * S)
+            shares = [(i, bufs[i].tobytes()) for i in ids]
+            if cnt == k:
+                ref_rc, ref = oracle.decode(E, k, n, shares)
+                stats["decode_k"] += 1
+            else:
+                ref_rc, ref = oracle.decode_correct(E, k, n, shares)
+                stats["decode_more"] += 1
+            if pinned_dst:
+                lib.rs_pinned_free(dp)
+            if arena is not None:
+                arena.free()
+            assert (rc == 0) == (ref_rc == 0), f"{case} cnt={cnt} corrupt={corrupt} rc {rc} vs oracle {ref_rc}"
+            if rc == 0:
+                assert got == ref, f"{case} cnt={cnt} corrupt={corrupt} decode bytes"
+                assert got == data.tobytes(), f"{case} cnt={cnt} corrupt={corrupt} not the message"
+        except AssertionError as e:
+            stats["failures"] += 1
+            if len(first) < 5:
+                first.append(str(e))
+    for fc in fecs.values():
+        fc.close()
+    stats["seconds"] = round(time.time() - t0, 1)
+    stats["first_failures"] = first
+    return stats
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=None)
+    ap.add_argument("--cases", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args()
+    if a.seconds is None and a.cases is None:
+        a.seconds = 120.0
+    st = run(a.seconds, a.cases, a.seed)
+    print(json.dumps(st))
+    return 1 if st["failures"] else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
