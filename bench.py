@@ -472,6 +472,29 @@ def config1_leg(local, reps=50):
     if not np.array_equal(dst_a, blob_np) or f.stat(f.STAT_DECODES_IN_PLACE) <= in0:
         raise RuntimeError("config1: the arena decode did not run in place or did not return the blob")
     arena.free()
+    # Receive batching (rs_decode_batch, one GPU pass for many messages --
+    # the engine's answer to one call per message): 64 config-1 messages,
+    # each with its own 4 seeded drops, survivors read from the caller's
+    # pageable shards, per-message time.
+    B = 64
+    brng = np.random.default_rng(0xBA7C)
+    bkeeps = [sorted(set(range(n)) - set(int(v) for v in brng.choice(n, size=4, replace=False))) for _ in range(B)]
+    base = {i: (blob_np.ctypes.data + i * S if i < k else parity.ctypes.data + (i - k) * S) for i in range(n)}
+    bdst = [np.zeros(L, dtype=np.uint8) for _ in range(B)]
+    bcounts = (ctypes.c_int * B)(*[k] * B)
+    bnums = (ctypes.c_int * (B * k))(*[i for kp in bkeeps for i in kp])
+    bptrs = (ctypes.c_void_p * (B * k))(*[base[i] for kp in bkeeps for i in kp])
+    bout = (ctypes.c_void_p * B)(*[d.ctypes.data for d in bdst])
+    bst = (ctypes.c_int * B)()
+
+    def dec_batch():
+        rc = lib.rs_decode_batch(f.handle, B, bcounts, bnums, bptrs, S, bout, bst)
+        if rc or any(bst):
+            raise RuntimeError(f"config1: rs_decode_batch returned {rc} / {list(bst)[:4]}")
+    batch_ms = _median_ms(dec_batch, max(5, reps // 5)) / B
+    if not all(np.array_equal(d, blob_np) for d in bdst):
+        raise RuntimeError("config1: rs_decode_batch did not return the blob")
+    del bdst
     # plugin mirror: prepareShards -> 14 Shards; 10 Receives, the last decodes
     blob = blob_np.tobytes()
     me = h.PeerID("tcp://localhost:3000", b"\x11" * 32)
@@ -536,15 +559,18 @@ def config1_leg(local, reps=50):
         "codec": {"encode_ms": enc_ms, "decode4_ms": dec_ms,
                   "encode_GBps": round(L * n / k / enc_ms / 1e6, 2),
                   "decode4_arena_ms": dec_arena_ms,
+                  "decode4_batch64_ms_per_message": round(batch_ms, 4),
                   "note": "caller-owned pageable buffers (what cgo passes), staged through pinned memory; "
-                          "decode4_arena: the survivors in an engine-pinned rs_arena, read in place"},
+                          "decode4_arena: the survivors in an engine-pinned rs_arena, read in place; "
+                          "decode4_batch64: 64 messages (own drops each) in one rs_decode_batch call"},
         "plugin": {"prepareShards_ms": prep_ms, "receive10_then_decode_ms": recv_ms,
                    "note": "C++ ShardPlugin mirror through pybind (blob and 14 shards copied across the "
                            "binding); no signer / verifier"},
         "cpu_1t": cpu,
         "gpu_vs_1core": {"encode": round(best["encode_ms"] / enc_ms, 3),
                          "decode4": round(min(v["decode4_ms"] for v in cpu.values()) / dec_ms, 3),
-                         "decode4_arena": round(min(v["decode4_ms"] for v in cpu.values()) / dec_arena_ms, 3)},
+                         "decode4_arena": round(min(v["decode4_ms"] for v in cpu.values()) / dec_arena_ms, 3),
+                         "decode4_batch64": round(min(v["decode4_ms"] for v in cpu.values()) / batch_ms, 3)},
     }
 
 

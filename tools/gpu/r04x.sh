@@ -1,0 +1,13 @@
+#!/bin/bash
+# config1 leg with receive batching (64 messages per rs_decode_batch call):
+# the bench GPU tests, then the default line.
+set -o pipefail
+O=gpurun_out/r04x
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_bench.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 3; }
+python3 -c "
+import json; d=json.load(open('$O/bench.json')); print(d['value'], d['roofline']['frac'], json.dumps(d['config1']['codec']), json.dumps(d['config1']['cpu_1t']['avx2_1t']), json.dumps(d['config1']['gpu_vs_1core']))"
+echo done
