@@ -1012,18 +1012,11 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
     return true;
 }
 
-// rs_decode of exactly k distinct shares that all lie in engine-pinned
-// memory (pinned.hpp: an rs_arena / rs_pinned_alloc range, 16-byte aligned,
-// readable up to round_up(S, 16)): the split-table kernel reads the
-// survivors over PCIe where they are, through a one-stripe shard table that
-// sits with the one-pattern table in the lease's pinned staging (read in
-// place too: nothing is uploaded).  The regenerated data shares go straight
-// into dst when dst is engine-pinned as well, else through pinned staging;
-// the present ones are copied into dst on the host while the kernel runs.
-// Returns false (nothing done) when the shares are not all engine-pinned.
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
-// Rebuild's choice `surv` is read at device address dev[j]; the present data
-// shares are copied into dst (unless present_done) while the kernel runs.
+// Rebuild's choice `surv` is read at device address dev[j] (column chunk by
+// column chunk when nch > 1, `stage` filling each chunk's survivor columns
+// first); the present data shares are copied into dst (unless present_done)
+// while the kernel runs.
 using StageFn = std::function<void(size_t off, size_t w)>;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
@@ -1044,6 +1037,15 @@ int stage_chunks(size_t bytes) {
 }
 size_t chunk_off(size_t S, int c, int nch) { return c >= nch ? S : (S * c / nch) & ~size_t(15); }
 
+// rs_decode of exactly k distinct shares that all lie in engine-pinned
+// memory (pinned.hpp: an rs_arena / rs_pinned_alloc range, 16-byte aligned,
+// readable up to round_up(S, 16)): the split-table kernel reads the
+// survivors over PCIe where they are, through a one-stripe shard table that
+// sits with the one-pattern table in the lease's pinned staging (read in
+// place too: nothing is uploaded).  The regenerated data shares go straight
+// into dst when dst is engine-pinned as well, else through pinned staging;
+// the present ones are copied into dst on the host while the kernel runs.
+// Returns false (nothing done) when the shares are not all engine-pinned.
 bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
                      const std::vector<const uint8_t*>& by_id, size_t S, uint8_t* dst, int* rc) {
     const int k = c->k;
