@@ -400,11 +400,14 @@ def config1_leg(local, reps=50):
     median of `reps` calls:
       * codec: rs_encode / rs_decode at the C ABI on caller-owned pageable
         buffers (what the cgo shim hands over; PCIe-inclusive);
-      * plugin: the C++ ShardPlugin mirror -- prepareShards into 14 Shard
-        messages (no signer), and the 10 surviving Shards received (pooled:
-        with m = 4 lost the reference's Receive never gets its k+1-th,
-        decode-triggering shard, main.go:65-72) then decoded with
-        FEC.Decode, through its Python binding;
+      * plugin: the C++ ShardPlugin mirror timed in C++
+        (host/plugin_latency.cpp, no binding in the timed region):
+        prepareShards into 14 Shards, those Shards marshalled the way
+        net.Broadcast sends them, ShardAndBroadcastWire (marshalled straight
+        from the encode output), and the 10 surviving Shards received
+        (pooled) plus an 11th arrival that decodes the pool (with m = 4 lost
+        the reference never gets a k+1-th shard, main.go:65-72: a resent
+        survivor plays it);
       * cpu: the oracle on 1 thread for the same blob (scalar mul_table and
         AVX2 split-nibble addmul: encode, and Rebuild of the dropped data
         shards).
@@ -495,32 +498,10 @@ def config1_leg(local, reps=50):
     if not all(np.array_equal(d, blob_np) for d in bdst):
         raise RuntimeError("config1: rs_decode_batch did not return the blob")
     del bdst
-    # plugin mirror: prepareShards -> 14 Shards; 10 Receives, the last decodes
+    # plugin mirror, timed in C++ (host/plugin_latency.cpp)
     blob = blob_np.tobytes()
-    me = h.PeerID("tcp://localhost:3000", b"\x11" * 32)
-    sender = h.NewShardPlugin(None, None, k, n)
-    wires = [s_.Marshal() for s_ in sender.prepareShards(me, blob)]
-    if len(wires) != n:
-        raise RuntimeError("config1: prepareShards did not return 14 shards")
-    prep_ms = _median_ms(lambda: sender.prepareShards(me, blob), reps)
-    msgs = []
-    for i in keep:
-        s_ = h.Shard()
-        s_.Unmarshal(wires[i])
-        msgs.append(s_)
-
-    hf = h.NewFEC(k, n)
-    shares = [h.Share(int(s_.ShardNumber), s_.ShardData) for s_ in msgs]
-
-    def receive():
-        r = h.NewShardPlugin(None, None, k, n)
-        for s_ in msgs:
-            if not r.Receive(me, s_).pooled:
-                raise RuntimeError("config1: a surviving shard was not pooled")
-        got, _ = hf.Decode(None, shares)
-        if got != blob:
-            raise RuntimeError("config1: the pooled shares did not decode to the blob")
-    recv_ms = _median_ms(receive, reps)
+    plug = h.plugin_latency(blob, k, n, lost, reps)
+    r4 = lambda v: round(v, 4)
     # The oracle on one thread, same blob.  Encode: parity only (infectious
     # emits the data shares as views).  Decode: what Decode does for dst --
     # the present data shares copied in, the dropped ones regenerated into
@@ -563,9 +544,18 @@ def config1_leg(local, reps=50):
                   "note": "caller-owned pageable buffers (what cgo passes), staged through pinned memory; "
                           "decode4_arena: the survivors in an engine-pinned rs_arena, read in place; "
                           "decode4_batch64: 64 messages (own drops each) in one rs_decode_batch call"},
-        "plugin": {"prepareShards_ms": prep_ms, "receive10_then_decode_ms": recv_ms,
-                   "note": "C++ ShardPlugin mirror through pybind (blob and 14 shards copied across the "
-                           "binding); no signer / verifier"},
+        "plugin": {"prepareShards_ms": r4(plug["prepareShards"]),
+                   "prepareShards_marshal_ms": r4(plug["prepareShards_marshal"]),
+                   "broadcast_wire_ms": r4(plug["broadcast_wire"]),
+                   "receive10_then_decode_ms": r4(plug["receive_then_decode"]),
+                   "receive10_copy_then_decode_ms": r4(plug["receive_copy_then_decode"]),
+                   "codec_encode_ms": r4(plug["codec_encode"]), "codec_decode4_ms": r4(plug["codec_decode"]),
+                   "memcpy_wire_ms": r4(plug["memcpy_wire"]), "wire_bytes": int(plug["wire_bytes"]),
+                   "note": "C++ ShardPlugin mirror timed in C++ (host/plugin_latency.cpp), medians; no signer / "
+                           "verifier. prepareShards_marshal = the reference's copies (DeepCopy main.go:255-258, then "
+                           "Marshal per Shard); broadcast_wire = ShardAndBroadcastWire, each share byte copied once "
+                           "into the wire; receive10_then_decode = 10 Receive(Shard&&) pooling + the decoding "
+                           "arrival; memcpy_wire = one copy of the 14 marshalled Shards"},
         "cpu_1t": cpu,
         "gpu_vs_1core": {"encode": round(best["encode_ms"] / enc_ms, 3),
                          "decode4": round(min(v["decode4_ms"] for v in cpu.values()) / dec_ms, 3),

@@ -175,10 +175,14 @@ __device__ __forceinline__ void bs_load(uint32_t (&x)[8], const uint8_t* shard, 
 }
 
 // Buffer-resource form (gen_bitslice -B): base and range in SGPRs, the lane
-// offset in one VGPR; num_records 0 makes every load return zeros.
+// offset in one VGPR; num_records 0 makes every load return zeros.  A present
+// input's range is the whole 32-bit offset space (num_records 0xFFFFFFFF):
+// rsmi.cpp accepts shards of up to 2^28 16-byte columns, so the last column
+// ends at 2^32 - 16 -- in range.  (0x7FFFFFFF, round 4, read zeros for every
+// column past 2 GiB; tests/test_gpu_parity.py test_bitslice_rec_past_2gib.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t bs_rsrc(const uint8_t* base, bool present) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), static_cast<short>(0),
-                                             present ? 0x7FFFFFFF : 0, 0x00020000);
+                                             present ? static_cast<int>(0xFFFFFFFFu) : 0, 0x00020000);
 }
 __device__ __forceinline__ void bs_load_buf(uint32_t (&x)[8], __amdgpu_buffer_rsrc_t r, uint32_t offa, uint32_t offb) {
     const bs_u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, offa, 0, 2);  // 2: nt
@@ -495,16 +499,25 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
     std::fprintf(f, "%s", R"(            er = sv_t ? (er & (er - 1ull)) : er;
         }
     }
-    // Tables while the first loads are in flight (read after the barrier;
-    // built once per block).
-    if (it == 0u)
-    for (uint32_t idx = threadIdx.x; idx < static_cast<uint32_t>(NG * R * TOP); idx += 256u) {
+)");
+    // The solve's coefficients are requested here, behind the first inputs'
+    // loads, and turned into LDS tables only after the last input.  Building
+    // them here (round 4) needed the byte at once: vmcnt(0) drained the
+    // prefetch of every block before input PF's loads could issue -- a full
+    // memory latency per block, in the movement twin as well.
+    const int CPT = (NG * kRows * top + 255) / 256;  // coefficients per thread
+    std::fprintf(f, "    constexpr int CPT = %d;  // decode coefficients per thread\n", CPT);
+    std::fprintf(f, "%s", R"(    uint32_t tcoef[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const uint32_t idx = threadIdx.x + 256u * q;
         const uint32_t o = idx / TOP, t = T0 + (idx - o * TOP);
         uint32_t slot = 0u;
 #pragma unroll
         for (int u = 0; u < M; ++u) slot = t == static_cast<uint32_t>(u) ? slot_t[u] : slot;
-        const uint32_t c = (o < e && ((pmask >> t) & 1u)) ? a.coef[(static_cast<size_t>(pat) * M + o) * K + slot] : 0u;
-        gfd::build_tables(c, &mtab[o][t - T0][0]);
+        tcoef[q] = 0u;
+        if (it == 0u && idx < static_cast<uint32_t>(NG * R * TOP) && o < e && ((pmask >> t) & 1u))
+            tcoef[q] = a.coef[(static_cast<size_t>(pat) * M + o) * K + slot];
     }
 )");
     for (int j = 0; j < N; ++j) {
@@ -545,6 +558,17 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
         }
         std::fprintf(f, "    }\n");
     }
+    // The solve's split tables (coefficients requested in the prologue).
+    std::fprintf(f, "%s", R"(    BS_FENCE();
+    if (it == 0u) {
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const uint32_t idx = threadIdx.x + 256u * q;
+            const uint32_t o = idx / TOP, t = idx - o * TOP;
+            if (idx < static_cast<uint32_t>(NG * R * TOP)) gfd::build_tables(tcoef[q], &mtab[o][t][0]);
+        }
+    }
+)");
     if (kMovementOnly) {
         // movement twin: output r stores accumulator row r mod TOP (same
         // stores, descriptors and mask record as the real kernel).
@@ -571,7 +595,7 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
 }
 
 )");
-    } else
+    } else {
     std::fprintf(f, "%s", R"(    BS_FENCE();
     if (it == 0u) __syncthreads();  // mtab complete
     // The parity outputs' q rows back to bytes (syndrome rows already are).
@@ -698,6 +722,7 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
 }
 
 )");
+    }  // the solve (not in the movement twin)
     std::fprintf(f,
                  "hipError_t launch_%s(const BitsliceRecArgs& a, hipStream_t stream) {\n"
                  "    const uint64_t blocks = a.count * a.blocks_per_stripe;\n"

@@ -2,6 +2,7 @@
 #include "host_pipeline.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -26,20 +27,50 @@ int pool_threads() {
 }
 }  // namespace
 
+namespace {
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#elif defined(__aarch64__)
+    asm volatile("yield");
+#endif
+}
+}  // namespace
+
+// Polled completion, bounded: a thread polls only while its
+// previous wait was short (at most the spin window: single-message calls),
+// and at most max_spinners threads poll at once -- noise runs Receive once
+// per peer connection, and each extra poller would burn a core for up to the
+// window.  Everything else blocks in hipEventSynchronize.
 hipError_t wait_event(hipEvent_t ev) {
     static const int spin_us = [] {
         const char* e = std::getenv("RSMI_SYNC_SPIN_US");
         return e ? std::max(0, std::min(std::atoi(e), 100000)) : 200;
     }();
-    if (spin_us > 0) {
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
-        do {
-            const hipError_t q = hipEventQuery(ev);
-            if (q != hipErrorNotReady) return q;
-            __builtin_ia32_pause();
-        } while (std::chrono::steady_clock::now() < until);
+    static const int max_spinners = [] {
+        const char* e = std::getenv("RSMI_SYNC_SPINNERS");
+        return e ? std::max(0, std::atoi(e)) : 2;
+    }();
+    static std::atomic<int> spinners{0};
+    thread_local bool last_short = true;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (spin_us > 0 && last_short) {
+        if (spinners.fetch_add(1, std::memory_order_relaxed) < max_spinners) {
+            const auto until = t0 + std::chrono::microseconds(spin_us);
+            do {
+                const hipError_t q = hipEventQuery(ev);
+                if (q != hipErrorNotReady) {
+                    spinners.fetch_sub(1, std::memory_order_relaxed);
+                    return q;
+                }
+                cpu_relax();
+            } while (std::chrono::steady_clock::now() < until);
+        }
+        spinners.fetch_sub(1, std::memory_order_relaxed);
     }
-    return hipEventSynchronize(ev);
+    const hipError_t r = hipEventSynchronize(ev);
+    last_short = std::chrono::steady_clock::now() - t0 <= std::chrono::microseconds(spin_us);
+    return r;
 }
 
 // ------------------------------------------------------------ CopyPool ----
@@ -83,7 +114,7 @@ void CopyPool::worker() {
             lk.unlock();
             const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
             while (queued_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
-                __builtin_ia32_pause();
+                cpu_relax();
             lk.lock();
         }
         cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });

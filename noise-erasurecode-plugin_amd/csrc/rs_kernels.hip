@@ -159,9 +159,29 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     const uint32_t* dstid = a.dst + static_cast<size_t>(pat) * a.dst_stride + row0;
     uint8_t* sp[kRegPtrs ? K : 1];
     if constexpr (kRegPtrs) {
+        // All K survivor ids in one batch of scalar loads, then all K
+        // addresses (pointer mode: one more batch): the mode branches sit
+        // outside the loops.  Round 4 resolved the survivors one at a time
+        // (id load, wait, mode branch, address load, wait): K dependent
+        // scalar round trips before the first survivor load.
+        uint32_t ids[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j)
-            sp[j] = uniform_ptr(shard(srcid ? __builtin_amdgcn_readfirstlane(srcid[j]) : static_cast<uint32_t>(j)));
+        for (int j = 0; j < K; ++j) ids[j] = static_cast<uint32_t>(j);
+        if (srcid) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ids[j] = __builtin_amdgcn_readfirstlane(srcid[j]);
+        }
+        if (a.shard_ptrs) {
+            const uint64_t* tp = a.shard_ptrs + s * (a.k + a.m);
+#pragma unroll
+            for (int j = 0; j < K; ++j) sp[j] = uniform_ptr(reinterpret_cast<uint8_t*>(tp[ids[j]]));
+        } else {
+            uint8_t* dbase = a.data + s * a.data_ss;
+            uint8_t* pbase = a.parity + s * a.parity_ss - static_cast<uint64_t>(K) * a.pitch;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                sp[j] = (ids[j] < static_cast<uint32_t>(K) ? dbase : pbase) + static_cast<uint64_t>(ids[j]) * a.pitch;
+        }
     } else {
         for (int i = threadIdx.x; i < k; i += BT) sptr[i] = shard(srcid ? srcid[i] : static_cast<uint32_t>(i));
     }
@@ -185,12 +205,27 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     // ids, so whole 4-id groups load unconditionally (s_load_dwordx4); rows
     // past eg point at a valid shard and are never stored.
     uint8_t* dp[TG * 4];
+    {
+        uint32_t oid[TG * 4];
 #pragma unroll
-    for (int g = 0; g < TG; ++g) {
-        const uint4 ids = *reinterpret_cast<const uint4*>(dstid + 4 * g);
-        const uint32_t idv[4] = {ids.x, ids.y, ids.z, ids.w};
+        for (int g = 0; g < TG; ++g) {
+            const uint4 ids = *reinterpret_cast<const uint4*>(dstid + 4 * g);
+            oid[4 * g + 0] = __builtin_amdgcn_readfirstlane(ids.x);
+            oid[4 * g + 1] = __builtin_amdgcn_readfirstlane(ids.y);
+            oid[4 * g + 2] = __builtin_amdgcn_readfirstlane(ids.z);
+            oid[4 * g + 3] = __builtin_amdgcn_readfirstlane(ids.w);
+        }
+        if (a.shard_ptrs) {
+            const uint64_t* tp = a.shard_ptrs + s * (a.k + a.m);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dp[4 * g + r] = uniform_ptr(shard(__builtin_amdgcn_readfirstlane(idv[r])));
+            for (int r = 0; r < TG * 4; ++r) dp[r] = uniform_ptr(reinterpret_cast<uint8_t*>(tp[oid[r]]));
+        } else {
+            uint8_t* dbase = a.data + s * a.data_ss;
+            uint8_t* pbase = a.parity + s * a.parity_ss - static_cast<uint64_t>(a.k) * a.pitch;
+#pragma unroll
+            for (int r = 0; r < TG * 4; ++r)
+                dp[r] = (oid[r] < a.k ? dbase : pbase) + static_cast<uint64_t>(oid[r]) * a.pitch;
+        }
     }
     // Split tables of rows [row0, row0 + MG): sub-step (j, g) holds rows
     // 4g..4g+3 as 4 x 5 dwords.

@@ -654,6 +654,14 @@ void wait_patterns(rs_ctx* c, hipStream_t s) {
 // caller behind that backlog.
 // Returns whether it waited; the caller commits the lease's watermark
 // (seen_patterns) only after L.end(s), so a failed launch leaves no claim.
+// Skipping the wait is sound only while three invariants hold (ADVICE r04;
+// tests/test_gpu_concurrency.py test_watermark_reuse_while_tables_move):
+//   1. launch_reconstruct holds pat_mu from this wait until L.end(s), so no
+//      build, growth or eviction can slip between the check and the launch;
+//   2. a lease's dev_pending is never cleared, so L.begin(s) always orders s
+//      after the lease's previous launch (which followed the rows it read);
+//   3. every move of the device tables (growth copy, eviction rebuild) bumps
+//      tables_gen, so a moved table never passes the first test below.
 bool wait_patterns_for(rs_ctx* c, Lease& L, size_t max_pid, hipStream_t s) {
     if (L.seen_tables == c->tables_gen && max_pid < L.seen_uploaded) return false;
     wait_patterns(c, s);
@@ -1012,12 +1020,26 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
     return true;
 }
 
+// Whether [dst, dst + len) meets any of the survivors by_id[surv[j]] (S bytes each).
+bool ranges_overlap(const uint8_t* dst, size_t len, const std::vector<const uint8_t*>& by_id,
+                    const std::vector<int>& surv, size_t S) {
+    const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst), d1 = d0 + len;
+    for (int id : surv) {
+        const uintptr_t s0 = reinterpret_cast<uintptr_t>(by_id[id]), s1 = s0 + S;
+        if (s0 < d1 && d0 < s1) return true;
+    }
+    return false;
+}
+
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
 // Rebuild's choice `surv` is read at device address dev[j] (column chunk by
 // column chunk when nch > 1, `stage` filling each chunk's survivor columns
 // first); the present data shares are copied into dst (unless present_done)
-// while the kernel runs.
+// while the kernel runs -- or after it, when dst overlaps a survivor the
+// kernel reads in place.  Returns kDecodeNoStaging, having done nothing, when
+// its pinned staging cannot be had (the caller falls back to the pipeline).
 using StageFn = std::function<void(size_t off, size_t w)>;
+constexpr int kDecodeNoStaging = -1000;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
                   bool present_done, int nch = 1, const StageFn& stage = nullptr);
@@ -1059,7 +1081,9 @@ bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
         dev[j] = rsmi::pinned_device_address(p, span);
         if (!dev[j]) return false;
     }
-    *rc = decode_launch(c, L, present, by_id, surv, dev, S, dst, false);
+    const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false);
+    if (r == kDecodeNoStaging) return false;
+    *rc = r;
     ++c->decodes_in_place;
     return true;
 }
@@ -1088,8 +1112,10 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     auto stage = [&](size_t off, size_t w) {
         for (int j = 0; j < k; ++j) std::memcpy(st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w);
     };
-    *rc = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
-                        stage_chunks(static_cast<size_t>(k) * S), stage);
+    const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
+                                stage_chunks(static_cast<size_t>(k) * S), stage);
+    if (r == kDecodeNoStaging) return false;
+    *rc = r;
     return true;
 }
 
@@ -1105,12 +1131,16 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     auto copy_present = [&] {
         if (present_done) return;
         for (int i = 0; i < k; ++i)
-            if (present[i]) std::memcpy(dst + static_cast<size_t>(i) * S, by_id[i], S);
+            if (present[i]) std::memmove(dst + static_cast<size_t>(i) * S, by_id[i], S);
     };
     if (e == 0) {
         copy_present();
         return RS_OK;
     }
+    // A caller's dst may hold survivors (infectious lets shares alias dst):
+    // then the present shares are copied only after the kernel has read them
+    // (ADVICE r04).  Staged survivors (stage != null) are copies already.
+    const bool overlap = !stage && ranges_overlap(dst, static_cast<size_t>(k) * S, by_id, surv, S);
     std::vector<uint8_t> rows;
     if (!rsmi::decode_rows(c->enc, k, c->n, surv, missing, rows)) return RS_ESINGULAR;
     nch = std::max(1, std::min(nch, static_cast<int>(std::min<size_t>(kBatchChunks, S / 4096))));  // >= 4 KiB a chunk
@@ -1118,11 +1148,11 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     // 16-byte aligned), else rows of the lease's pinned output staging.
     const bool dst_direct = !(S & 15u) && !(reinterpret_cast<uintptr_t>(dst) & 15u) &&
                             rsmi::pinned_device_address(dst, static_cast<size_t>(k) * S) != 0;
-    if (!dst_direct && !L.st_out.acquire(static_cast<size_t>(e) * span)) return RS_ENOMEM;
+    if (!dst_direct && !L.st_out.acquire(static_cast<size_t>(e) * span)) return kDecodeNoStaging;
     // Pinned staging: [one-pattern table][nch shard tables: k survivors, e outputs]
     const size_t pbytes = PatLayout(c, 1).total, toff = round_up(pbytes, 16);
     const size_t n8 = static_cast<size_t>(c->n) * 8;
-    if (!L.st_onepat.acquire(toff + nch * n8)) return RS_ENOMEM;
+    if (!L.st_onepat.acquire(toff + nch * n8)) return kDecodeNoStaging;
     uint8_t* host = static_cast<uint8_t*>(L.st_onepat.p);
     std::vector<uint8_t> coef(static_cast<size_t>(c->m) * k, 0);
     std::copy(rows.begin(), rows.end(), coef.begin());
@@ -1167,7 +1197,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
         if (err == hipSuccess) ++launched;
     }
     L.end(s);
-    copy_present();  // while the kernel runs
+    if (!overlap) copy_present();  // while the kernel runs
     for (int ch = 0; ch < launched; ++ch) {
         const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
         if (err == hipSuccess) err = w8;
@@ -1178,6 +1208,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                         static_cast<uint8_t*>(L.st_out.p) + t * span + off, w);
     }
     if (launched < nch) (void)rsmi::wait_event(L.dev_done);  // a failed launch: drain what was queued
+    if (overlap && err == hipSuccess) copy_present();
     return err == hipSuccess ? RS_OK : RS_EDEVICE;
 }
 
@@ -1243,9 +1274,17 @@ int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
     auto copy_present = [&] {
         std::vector<rsmi::CopyPool::Piece> pieces;
         for (int i = 0; i < k; ++i)
-            if (present[i]) pieces.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
+            if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i])
+                pieces.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
         rsmi::CopyPool::shared().run(pieces);
     };
+    // dst holding survivors: the pipeline stages them chunk by chunk while
+    // the overlap hook would run, so the copy waits for the GPU rows.
+    if (ranges_overlap(dst, static_cast<size_t>(k) * S, by_id, surv, S)) {
+        const int rc = gpu_rows(c, L, surv, sp, missing, outs, S);
+        if (rc == RS_OK) copy_present();
+        return rc;
+    }
     return gpu_rows(c, L, surv, sp, missing, outs, S, copy_present);
 }
 

@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "infectious.hpp"
+#include "plugin_latency.hpp"
 #include "shard_plugin.hpp"
 
 namespace py = pybind11;
@@ -193,6 +194,29 @@ PYBIND11_MODULE(_rsmi_host, m) {
                  const std::vector<uint8_t> v = to_vec(input);
                  check(p.ShardAndBroadcast(self, &v, [&](const Shard& s) { broadcast(s); }));
              })
+        .def("ShardAndBroadcastWire",
+             [](ShardPlugin& p, const PeerID& self, py::object input, const std::function<void(py::bytes)>& broadcast) {
+                 if (input.is_none()) {
+                     check(p.ShardAndBroadcastWire(self, nullptr, [](const uint8_t*, size_t) {}));
+                     return;
+                 }
+                 const std::vector<uint8_t> v = to_vec(input.cast<py::bytes>());
+                 check(p.ShardAndBroadcastWire(self, &v, [&](const uint8_t* w, size_t len) {
+                     broadcast(py::bytes(reinterpret_cast<const char*>(w), len));
+                 }));
+             })
+        .def("ReceiveMove",
+             [](ShardPlugin& p, const PeerID& sender, Shard msg) {
+                 // Receive(Shard&&): the pooled share keeps the message's bytes
+                 ReceiveEvent ev;
+                 Status st;
+                 {
+                     py::gil_scoped_release nogil;
+                     st = p.Receive(sender, std::move(msg), &ev);
+                 }
+                 check(st);
+                 return ev;
+             })
         .def("shardInput",
              [](ShardPlugin& p, const py::bytes& input) {
                  std::vector<Share> out;
@@ -224,6 +248,19 @@ PYBIND11_MODULE(_rsmi_host, m) {
     m.def("serializeMessage", [](const PeerID& id, const py::bytes& msg) {
         return to_bytes(serializeMessage(id, to_vec(msg)));
     });
+    m.def("plugin_latency",
+          [](const py::bytes& blob, int k, int n, const std::vector<int>& dropped, int reps) {
+              const std::vector<uint8_t> b = to_vec(blob);
+              std::map<std::string, double> out;
+              Status st;
+              {
+                  py::gil_scoped_release nogil;
+                  st = PluginLatency(b, k, n, dropped, reps, &out);
+              }
+              check(st);
+              return out;
+          },
+          "The config-1 plugin path timed in C++ (plugin_latency.cpp): median ms per step.");
     m.def("largestPrimeFactors", &largestPrimeFactors);
     m.def("StatusText", &StatusText);
 }

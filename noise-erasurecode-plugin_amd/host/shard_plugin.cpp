@@ -152,27 +152,34 @@ Status ShardPlugin::shardInput(const std::vector<uint8_t>& input, std::vector<Sh
     return Status::Ok();
 }
 
-Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
-                                  std::vector<Shard>* out) {
-    if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
-    // The signature hash (main.go:219-223) and the encode (main.go:225) are
-    // independent: a helper thread hashes (one message: host CPU, no HIP
-    // calls) while this thread, whose HIP state is warm, drives the GPU
-    // encode, so the call costs about the longer of the two, not their sum.
-    // The signer itself runs here, after both.
-    std::vector<Share> shares;
-    std::vector<uint8_t> sig;
+// The signature hash (main.go:219-223) and the encode (main.go:225) are
+// independent: a helper thread hashes (one message: host CPU, no HIP calls)
+// while this thread, whose HIP state is warm, drives the GPU encode, so the
+// call costs about the longer of the two, not their sum.  The signer itself
+// runs here, after both.
+Status ShardPlugin::sign_input(const PeerID& self, const std::vector<uint8_t>& input, std::vector<uint8_t>* sig,
+                               const std::function<Status()>& encode) {
     std::vector<std::vector<uint8_t>> h;
     std::future<Status> hashed;
     if (sign_) {
-        std::vector<std::vector<uint8_t>> ser{serializeMessage(self, *input)};
+        std::vector<std::vector<uint8_t>> ser{serializeMessage(self, input)};
         hashed = std::async(std::launch::async, [this, ser = std::move(ser), &h] { return HashBytes(ser, &h); });
     }
-    Status st = shardInput(*input, &shares);
+    Status st = encode();
     Status hs = sign_ ? hashed.get() : Status::Ok();
     if (!hs.ok()) return hs;
     if (!st.ok()) return st;
-    if (sign_) sig = sign_(h[0]);
+    if (sign_) *sig = sign_(h[0]);
+    return Status::Ok();
+}
+
+Status ShardPlugin::prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
+                                  std::vector<Shard>* out) {
+    if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
+    std::vector<Share> shares;
+    std::vector<uint8_t> sig;
+    Status st = sign_input(self, *input, &sig, [&] { return shardInput(*input, &shares); });
+    if (!st.ok()) return st;
     out->clear();
     for (Share& s : shares) {
         Shard m;
@@ -230,7 +237,55 @@ Status ShardPlugin::ShardAndBroadcast(const PeerID& self, const std::vector<uint
     return Status::Ok();
 }
 
+Status ShardPlugin::ShardAndBroadcastWire(const PeerID& self, const std::vector<uint8_t>* input,
+                                          const std::function<void(const uint8_t*, size_t)>& broadcast) {
+    if (input == nullptr) return Status::Err(RS_EINVAL, "network: input is null");
+    std::shared_ptr<FEC> f;
+    Status st = CachedFEC(MinimumNeededShards, TotalShards, &f);
+    if (!st.ok()) return st;
+    const size_t k = static_cast<size_t>(MinimumNeededShards), n = static_cast<size_t>(TotalShards);
+    if (input->size() % k != 0)
+        return Status::Err(RS_ELEN_NOT_MULTIPLE, std::string("Encode: ") + rs_strerror(RS_ELEN_NOT_MULTIPLE));
+    const size_t S = input->size() / k;
+    std::lock_guard<std::mutex> lk(wire_mu_);
+    wire_parity_.resize((n - k) * S);
+    // The parity goes into this plugin's buffer while the signature hash
+    // runs (sign_input); nothing is marshalled before the signature exists.
+    std::vector<uint8_t> sig;
+    st = sign_input(self, *input, &sig, [&] {
+        if (S == 0 || n == k) return Status::Ok();
+        const int rc = rs_encode(f->ctx(), input->data(), input->size(), wire_parity_.data());
+        return rc == RS_OK ? Status::Ok() : Status::Err(rc, std::string("Encode: ") + rs_strerror(rc));
+    });
+    if (!st.ok()) return st;
+    for (size_t i = 0; i < n; ++i) {
+        rs_shard_view v{};
+        v.file_signature = sig.data();
+        v.file_signature_len = sig.size();
+        v.shard_data = i < k ? input->data() + i * S : wire_parity_.data() + (i - k) * S;
+        v.shard_data_len = S;
+        v.shard_number = i;
+        v.total_shards = n;
+        v.minimum_needed_shards = k;
+        const size_t need = rs_shard_size(&v);
+        if (wire_.size() < need) wire_.resize(need);
+        size_t w = 0;
+        rs_shard_marshal(&v, wire_.data(), wire_.size(), &w);
+        broadcast(wire_.data(), w);
+    }
+    return Status::Ok();
+}
+
 Status ShardPlugin::Receive(const PeerID& sender, const Shard& msg, ReceiveEvent* ev) {
+    return receive(sender, msg, nullptr, ev);
+}
+
+Status ShardPlugin::Receive(const PeerID& sender, Shard&& msg, ReceiveEvent* ev) {
+    return receive(sender, msg, &msg.ShardData, ev);
+}
+
+// take: the message's bytes may be moved into the pool (Receive(Shard&&)).
+Status ShardPlugin::receive(const PeerID& sender, const Shard& msg, std::vector<uint8_t>* take, ReceiveEvent* ev) {
     ReceiveEvent local;
     ReceiveEvent& e = ev ? *ev : local;
     e = ReceiveEvent{};
@@ -248,7 +303,8 @@ Status ShardPlugin::Receive(const PeerID& sender, const Shard& msg, ReceiveEvent
             // (another Receive may have changed it meanwhile, as the
             // reference's Load/Delete/Store sequence allows).
             lk.unlock();
-            mine = std::make_shared<const Share>(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
+            mine = take ? std::make_shared<const Share>(Share{static_cast<int>(msg.ShardNumber), std::move(*take)})
+                        : std::make_shared<const Share>(Share{static_cast<int>(msg.ShardNumber), msg.ShardData});
             lk.lock();
             it = shards_.find(key);
             if (it == shards_.end() ||

@@ -96,6 +96,10 @@ public:
     // the decode of the pool (without itself being added), a pool holding
     // more than TotalShards is an error.
     Status Receive(const PeerID& sender, const Shard& msg, ReceiveEvent* ev = nullptr);
+    // The same for a message the caller hands over: a pooled shard keeps the
+    // message's ShardData (moved, not copied), as the reference's Share
+    // aliases shard.ShardData (main.go:57-69).
+    Status Receive(const PeerID& sender, Shard&& msg, ReceiveEvent* ev = nullptr);
 
     // Receive for a batch of arrivals (receive-side batching, SURVEY.md §8f
     // rank 3): the same pooling rules and per-key order as calling Receive on
@@ -109,6 +113,15 @@ public:
     // main.go:201-210 with net.Broadcast replaced by `broadcast`.
     Status ShardAndBroadcast(const PeerID& self, const std::vector<uint8_t>* input,
                              const std::function<void(const Shard&)>& broadcast);
+    // ShardAndBroadcast with the Shards marshalled (what net.Broadcast sends,
+    // shard.pb.go:219-252) straight from the encode's output -- the data
+    // shares from the input, the parity from the plugin's parity buffer --
+    // into one reused wire buffer: each share byte is copied once, where the
+    // reference copies it twice (DeepCopy main.go:255-258, then Marshal).
+    // broadcast gets each message's wire bytes, valid during the call; calls
+    // on one plugin serialise on the buffers.
+    Status ShardAndBroadcastWire(const PeerID& self, const std::vector<uint8_t>* input,
+                                 const std::function<void(const uint8_t* wire, size_t len)>& broadcast);
     // main.go:211-241 (input == nullptr -> "network: input is null").
     Status prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
                          std::vector<Shard>* out);
@@ -127,6 +140,9 @@ public:
     Status HashBytes(const std::vector<std::vector<uint8_t>>& msgs, std::vector<std::vector<uint8_t>>* out) const;
 
 private:
+    Status sign_input(const PeerID& self, const std::vector<uint8_t>& input, std::vector<uint8_t>* sig,
+                      const std::function<Status()>& encode);
+    Status receive(const PeerID& sender, const Shard& msg, std::vector<uint8_t>* take, ReceiveEvent* ev);
     Signer sign_;
     Verifier verify_;
     mutable std::mutex mu_;
@@ -136,6 +152,9 @@ private:
     // (main.go:72-77 decodes the pool's own backing array).
     using PoolEntry = std::shared_ptr<const Share>;
     std::unordered_map<std::string, std::vector<PoolEntry>> shards_;
+    std::mutex wire_mu_;
+    std::vector<uint8_t> wire_;         // ShardAndBroadcastWire's marshal buffer (grown, never shrunk)
+    std::vector<uint8_t> wire_parity_;  // ... and its parity shares
 };
 
 // NewShardPlugin(signaturePolicy, hashPolicy, k, n)  main.go:108-115;

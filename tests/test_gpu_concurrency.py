@@ -213,6 +213,76 @@ def test_pattern_cache_eviction_without_sync():
     f.close()
 
 
+@pytest.mark.parametrize("cap", [None, "40"])
+def test_watermark_reuse_while_tables_move(cap):
+    """launch_reconstruct skips its wait for the pattern builds
+    when every pattern it reads is older than its lease's watermark and the
+    tables have not moved (rsmi.cpp wait_patterns_for).  One thread reuses a
+    fixed, long-cached pattern set over and over while another meets fresh
+    patterns on every call, growing the device tables (cap None) or evicting
+    and rebuilding them (cap 40); with two leases the callers keep trading
+    leases.  Every reconstruct of both threads equals the originals."""
+    k, n, S = 64, 80, 4096
+    m = n - k
+    env = {"RSMI_MAX_LEASES": "2"}
+    if cap:
+        env["RSMI_PATTERN_CAP"] = cap
+    f = _fec_env(k, n, **env)
+    stripes = [8, 48]  # reuser, builder
+    bufs = []
+    for t in range(2):
+        data = torch.empty(stripes[t] * k * S, dtype=torch.uint8, device="cuda")
+        parity = torch.empty(stripes[t] * m * S, dtype=torch.uint8, device="cuda")
+        f.fill_splitmix(data.data_ptr(), data.numel(), 70 + t)
+        f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes[t])
+        bufs.append((data, parity))
+    f.sync()
+    refs = [(d.clone(), p.clone()) for d, p in bufs]
+    fixed = np.zeros((stripes[0], n), dtype=np.uint8)
+    rng0 = np.random.default_rng(5)
+    for s in range(stripes[0]):
+        fixed[s, rng0.choice(n, size=int(rng0.integers(1, m + 1)), replace=False)] = 1
+    errors = []
+    seen = set()  # the builder's distinct patterns
+
+    def worker(t):
+        rng = np.random.default_rng(200 + t)
+        data, parity = bufs[t]
+        d0, p0 = refs[t]
+        st = stripes[t]
+        stream = torch.cuda.Stream()
+        with torch.cuda.stream(stream):
+            for it in range(30):
+                if t == 0:
+                    er = fixed
+                else:
+                    er = np.zeros((st, n), dtype=np.uint8)
+                    for s in range(st):
+                        er[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 1
+                    seen.update(row.tobytes() for row in er)
+                data.copy_(d0)
+                parity.copy_(p0)
+                data.view(st, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+                parity.view(st, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+                f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, st,
+                                      er.tobytes(), stream.cuda_stream)
+                stream.synchronize()
+                if not (torch.equal(data, d0) and torch.equal(parity, p0)):
+                    errors.append((t, it))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    if cap:
+        assert f.pattern_evictions() >= 10
+    else:
+        assert f.pattern_count() >= len(seen) > 1000  # every pattern kept: the tables grew again and again
+    f.close()
+
+
 def test_rs_free_releases_lease_buffers():
     """rs_free must free every lease's device and pinned buffers
     (the rs_decode_batch workspaces included).  Three create / batch-decode

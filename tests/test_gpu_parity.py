@@ -393,6 +393,52 @@ def _check_ptrs_roundtrip(f, k, n, S, er, seed):
     assert torch.equal(pool[rows.view(-1), :S].view(stripes, n, S), full)
 
 
+@pytest.mark.parametrize("k,n", [(8, 14), (64, 80)])
+def test_bitslice_rec_past_2gib(k, n):
+    """the syndrome kernel's buffer loads gave a present
+    input a 0x7FFFFFFF-byte range, so every column at or past 2 GiB read as
+    zeros while rs_reconstruct_* accept shards up to 2^28 columns.  One
+    pointer-mode stripe of (2^31 + 8,232)-byte shards: survivor i is the
+    window of one random buffer starting at byte 16*i (distinct bytes per
+    survivor, one allocation), data shards 1 and 5 erased.  The outputs at
+    sampled columns on both sides of 2 GiB and at the ragged end equal the
+    oracle's Rebuild of the same k survivors at those columns (Rebuild is
+    column-wise linear, so any bytes will do, codeword or not)."""
+    f = fec(k, n)
+    assert f.kernel_name(1).startswith("bitslice_rec")
+    m = n - k
+    S = (1 << 31) + 8192 + 40
+    Sp = (S + 15) // 16 * 16
+    X = torch.empty(Sp + 16 * n, dtype=torch.uint8, device="cuda")
+    f.fill_splitmix(X.data_ptr(), X.numel(), 4242)
+    erased = [1, 5]
+    outs = [torch.zeros(Sp, dtype=torch.uint8, device="cuda") for _ in erased]
+    table = [X.data_ptr() + 16 * i for i in range(n)]
+    for t, i in enumerate(erased):
+        table[i] = outs[t].data_ptr()
+    tab = torch.tensor(table, dtype=torch.int64, device="cuda")
+    er = np.zeros((1, n), dtype=np.uint8)
+    er[0, erased] = 1
+    f.reconstruct_ptrs(tab.data_ptr(), S, 1, er.tobytes())
+    f.sync()
+    c2g = 1 << 27  # the column at 2 GiB
+    cols = [0, 1, 511, 512, c2g - 513, c2g - 1, c2g, c2g + 1, c2g + 511, c2g + 512, Sp // 16 - 2, Sp // 16 - 1]
+    idx = torch.tensor([16 * c + b for c in cols for b in range(16)], dtype=torch.int64, device="cuda")
+    # Rebuild's survivors: the present data shards and, for the d erased
+    # data slots, the d highest-numbered parity shards.
+    surv = [i for i in range(k) if i not in erased] + list(range(n - 1, n - 1 - len(erased), -1))
+    shares = [(i, X[16 * i:][idx].cpu().numpy().tobytes()) for i in surv]
+    rc, ref = oracle.decode(oracle.fec_matrix(k, n), k, n, shares)
+    assert rc == 0
+    L = 16 * len(cols)
+    for t, i in enumerate(erased):
+        got = outs[t][idx].cpu().numpy().tobytes()
+        want = ref[i * L:(i + 1) * L]
+        # the ragged last column holds S % 16 = 8 real bytes; the rest is padding
+        assert got[:L - 8] == want[:L - 8], (k, n, i)
+    del X, outs
+
+
 def test_reconstruct_split_between_kernels():
     """RS(64,16) reconstruct with RSMI_BITSLICE_REC_MIN_E=5: stripes with
     e < 5 go to the split-table kernel, the rest to the syndrome kernel, in
@@ -898,6 +944,45 @@ def test_host_api_pinned_buffers(k, n, S):
     finally:
         for p in (pin_in, pin_par, pin_dst):
             lib.rs_pinned_free(p)
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("S", [4096, 104858, 300000])
+def test_decode_dst_overlapping_survivors(pinned, S):
+    """rs_decode copies the present data shares into dst while
+    the GPU reads the survivors -- in place when they are engine-pinned.  Here
+    the shares live INSIDE dst, one row later than their own (share i at row
+    i + 1), so copying share i to row i overwrites share i - 1 where the
+    kernel reads it; the engine must copy only after the kernel.  The decoded
+    bytes equal the original data (engine-pinned and pageable memory; staged,
+    chunked and pipelined sizes)."""
+    import ctypes
+    lib = rsmi.load()
+    k, n = 10, 14
+    m = n - k
+    f = fec(k, n)
+    data, sh = _shards(k, n, S, 4321 + S)
+    size = (n + 1) * S
+    buf = lib.rs_pinned_alloc(size) if pinned else None
+    keep_alive = None
+    if not pinned:
+        keep_alive = ctypes.create_string_buffer(size)
+        buf = ctypes.addressof(keep_alive)
+    assert buf
+    try:
+        for i in range(n):
+            ctypes.memmove(buf + (i + 1) * S, sh[i], S)
+        # data shares 0-3 lost: their outputs (rows 0-3) overwrite no survivor;
+        # copying present share i (row i + 1) to row i overwrites share i - 1
+        lost = [0, 1, 2, 3]
+        keep = [i for i in range(n) if i not in lost]
+        nums = (ctypes.c_int * k)(*keep)
+        ptrs = (ctypes.c_void_p * k)(*[buf + (i + 1) * S for i in keep])
+        assert lib.rs_decode(f.handle, nums, ptrs, k, S, buf) == rsmi.RS_OK
+        assert ctypes.string_at(buf, k * S) == data
+    finally:
+        if pinned:
+            lib.rs_pinned_free(buf)
 
 
 @pytest.mark.parametrize("S,pitch", [(100, 112), (65536, 65536), (4099, 4112)])

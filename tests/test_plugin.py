@@ -165,6 +165,65 @@ def test_config1_blob_rs10_4():
     assert got == blob
 
 
+@pytest.mark.parametrize("k,n,L", [(4, 6, 64), (10, 14, 1048580), (8, 14, 8 * 37)])
+def test_broadcast_wire_equals_marshalled_prepare_shards(k, n, L):
+    """ShardAndBroadcastWire (marshalled straight from the encode output, one
+    reused buffer) sends exactly the bytes of prepareShards' Shards marshalled
+    one by one (net.Broadcast, shard.pb.go:219-252), in share order, signed
+    the same way; the parity inside equals the oracle's."""
+    p = plugin(k, n)
+    msg = oracle.splitmix_bytes(L, k + n).tobytes()
+    want = [s.Marshal() for s in p.prepareShards(SELF, msg)]
+    got = []
+    p.ShardAndBroadcastWire(SELF, msg, got.append)
+    assert got == want
+    S = L // k
+    par = oracle.encode(oracle.fec_matrix(k, n), k, n, msg)
+    s = h.Shard()
+    s.Unmarshal(got[k])
+    assert s.ShardData == par[:S] and s.FileSignature == sign(h.serializeMessage(SELF, msg))
+    with pytest.raises(h.HostError):
+        p.ShardAndBroadcastWire(SELF, None, got.append)  # "network: input is null"
+    with pytest.raises(h.HostError):
+        p.ShardAndBroadcastWire(SELF, msg + b"x", got.append)  # len % k != 0
+
+
+def test_receive_move_pools_and_decodes():
+    """Receive(Shard&&) keeps the handed-over bytes in the pool (the
+    reference's Share aliases shard.ShardData, main.go:57-69): the same
+    pooling, decode and verification as Receive(const Shard&)."""
+    k, n = 10, 14
+    p = plugin(k, n)
+    msg = oracle.splitmix_bytes(10 * 1001, 9).tobytes()
+    shards = [x.Marshal() for x in p.prepareShards(SELF, msg)]
+    recv = plugin(k, n)
+    evs = []
+    for i in [13, 0, 2, 3, 5, 7, 8, 9, 11, 12, 4]:
+        s = h.Shard()
+        s.Unmarshal(shards[i])
+        evs.append(recv.ReceiveMove(SELF, s))
+    assert all(e.pooled for e in evs[:k])
+    assert evs[k].decoded and evs[k].verified and evs[k].message == msg
+
+
+def test_plugin_latency_harness():
+    """host/plugin_latency.cpp (bench.py's config1.plugin leg): the C++
+    timing harness runs every step on the config-1 blob, checks its own
+    outputs (decode == blob, wire broadcast == marshalled Shards, the
+    decoding Receive returns the blob) and reports positive medians."""
+    k, n = 10, 14
+    blob = oracle.splitmix_bytes(1 << 20, 0x5EED).tobytes() + b"\0" * 4
+    r = h.plugin_latency(blob, k, n, [1, 6, 11, 13], 5)
+    for key in ("codec_encode", "codec_decode", "shardInput", "prepareShards", "prepareShards_marshal",
+                "broadcast_wire", "receive_then_decode", "receive_copy_then_decode", "memcpy_wire"):
+        assert r[key] > 0, key
+    # per Shard: data (tag + 3-byte length) + number, total, k (2 bytes each);
+    # no signer, so no signature field; shard 0 omits its zero number
+    assert r["wire_bytes"] == 14 * (len(blob) // k) + 14 * (4 + 2 + 2 + 2) - 2
+    with pytest.raises(h.HostError):
+        h.plugin_latency(blob, k, n, [0, 1, 2, 3, 4], 5)  # 9 survivors
+
+
 def test_host_fec_api():
     f = h.NewFEC(8, 14)
     assert (f.Required(), f.Total()) == (8, 14)
