@@ -549,6 +549,7 @@ def config1_leg(local, reps=50):
                    "broadcast_wire_ms": r4(plug["broadcast_wire"]),
                    "receive10_then_decode_ms": r4(plug["receive_then_decode"]),
                    "receive10_copy_then_decode_ms": r4(plug["receive_copy_then_decode"]),
+                   "receive10_pool_ms": r4(plug["receive_pool10"]), "receive_trigger_ms": r4(plug["receive_trigger"]),
                    "codec_encode_ms": r4(plug["codec_encode"]), "codec_decode4_ms": r4(plug["codec_decode"]),
                    "memcpy_wire_ms": r4(plug["memcpy_wire"]), "wire_bytes": int(plug["wire_bytes"]),
                    "note": "C++ ShardPlugin mirror timed in C++ (host/plugin_latency.cpp), medians; no signer / "

@@ -69,6 +69,11 @@ struct BitsliceRecArgs {
     const uint8_t* zpage;        // 2 KiB (one wave window) loaded for absent inputs
     const uint64_t* shard_ptrs;  // [stripe][k + m] shard addresses (pointer mode), or nullptr
     uint32_t xcd;                // XCD-aware block order (xcd.hpp): stripes per region, 0 = natural
+    // Small reconstructs: stripe_desc == nullptr, the count <= kInlineDesc
+    // descriptors and their mask records in the kernel arguments (no upload).
+    static constexpr int kInlineDesc = 16;
+    uint2 inl_desc[kInlineDesc];
+    BsStripeMask inl_mask[kInlineDesc];
 };
 
 using BitsliceRecLaunch = hipError_t (*)(const BitsliceRecArgs&, hipStream_t);

@@ -387,9 +387,10 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
     const uint64_t sv = bx / a.blocks_per_stripe;
     const uint32_t blk = bx - static_cast<uint32_t>(sv) * a.blocks_per_stripe;
     // The descriptor and its mask record (below), both scalar loads issued
-    // back to back.
-    const BsStripeMask mk = a.stripe_mask[sv];
-    const uint2 desc = a.stripe_desc[sv];
+    // back to back -- from the uploaded arrays, or (a small call) from the
+    // kernel arguments.
+    const BsStripeMask mk = a.stripe_desc ? a.stripe_mask[sv] : a.inl_mask[sv];
+    const uint2 desc = a.stripe_desc ? a.stripe_desc[sv] : a.inl_desc[sv];
     const uint64_t s = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(desc.x));
     const uint32_t sw = __builtin_amdgcn_readfirstlane(desc.y);
     const uint32_t pat = sw >> 8, e = sw & 0xFFu;

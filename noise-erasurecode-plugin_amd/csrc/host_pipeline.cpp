@@ -51,10 +51,14 @@ hipError_t wait_event(hipEvent_t ev) {
         const char* e = std::getenv("RSMI_SYNC_SPINNERS");
         return e ? std::max(0, std::atoi(e)) : 2;
     }();
+    static const bool adaptive = [] {
+        const char* e = std::getenv("RSMI_SYNC_ADAPTIVE");  // 0: poll every wait (round 4; A/B)
+        return !(e && std::atoi(e) == 0);
+    }();
     static std::atomic<int> spinners{0};
     thread_local bool last_short = true;
     const auto t0 = std::chrono::steady_clock::now();
-    if (spin_us > 0 && last_short) {
+    if (spin_us > 0 && (last_short || !adaptive)) {
         if (spinners.fetch_add(1, std::memory_order_relaxed) < max_spinners) {
             const auto until = t0 + std::chrono::microseconds(spin_us);
             do {

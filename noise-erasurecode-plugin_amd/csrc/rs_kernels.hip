@@ -94,6 +94,26 @@ __device__ __forceinline__ void mac_step(uint32_t (&acc)[kRowsPerStep][4], const
     }
 }
 
+// mac_step for the first `rows` (1..4, wave-uniform) rows: one branch per
+// row past the first, around all four words.
+__device__ __forceinline__ void mac_step_rows(uint32_t (&acc)[kRowsPerStep][4], const uint4& x,
+                                              const uint32_t (&T)[kStepWords], int rows) {
+    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+    uint32_t ia[4], ib[4], ic[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        ia[w] = xw[w] & 0x07070707u;
+        ib[w] = (xw[w] >> 3) & 0x07070707u;
+        ic[w] = (xw[w] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int r = 0; r < kRowsPerStep; ++r) {
+        if (r > 0 && r >= rows) break;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[r][w] = gf_mac(acc[r][w], &T[r * 5], ia[w], ib[w], ic[w]);
+    }
+}
+
 // Step boundary: the accumulators of the finished sub-step are inputs of the
 // asm, so its arithmetic completes before the boundary, and the memory
 // clobber keeps the next sub-step's LDS reads after it.  At most two
@@ -112,6 +132,15 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     constexpr int TG = (MG + kRowsPerStep - 1) / kRowsPerStep;  // sub-steps per survivor
     constexpr int RL = MG - (TG - 1) * kRowsPerStep;            // rows in the last sub-step
     constexpr bool kRegPtrs = K > 0 && K <= 16;           // survivor bases kept in SGPRs
+    // A single 4-row group (the RS(10,4), RS(4,2), RS(8,14) reconstructs)
+    // codes only the stripe's e rows: one MG = 4 launch serves stripes of
+    // 1..4 erasures, and coding all 4 rows for each cost 1.6x the VALU of the
+    // 1..4 mix (e = 2.5 on average).
+#ifdef RSMI_NO_DYNROWS  // A/B builds only
+    constexpr bool kDynRows = false;
+#else
+    constexpr bool kDynRows = TG == 1 && RL == kRowsPerStep && kRegPtrs;
+#endif
     constexpr int JB = (K == 0) ? 8 : (K <= 16 ? K : 8);  // survivor loads in flight
     const int k = K ? K : static_cast<int>(a.k);
     extern __shared__ uint4 lds4[];
@@ -130,6 +159,7 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     // and survivor reads without a dependent read of host memory first.
     uint2 desc = make_uint2(static_cast<uint32_t>(sv), a.desc0 ? a.desc0 : a.m);
     if (a.stripe_desc) desc = a.stripe_desc[sv];
+    else if (a.n_inline) desc = a.inl_desc[sv];
     const uint64_t s = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(desc.x));
     const uint32_t sw = __builtin_amdgcn_readfirstlane(desc.y);
     const uint32_t pat = sw >> 8;
@@ -284,7 +314,9 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
                     const int step = (jb + q) * TG + g;
                     const bool more = (g + 1 < TG) || (q + 1 < JB && (K != 0 || jb + q + 1 < k));
                     if (more) load_step(lds4 + static_cast<size_t>(step + 1) * (kStepWords / 4), TB);
-                    if (TG == 1 || g < tg_used) {
+                    if constexpr (kDynRows) {
+                        mac_step_rows(acc[g], x[q], TA, eg);
+                    } else if (TG == 1 || g < tg_used) {
                         if (g == TG - 1) mac_step<RL>(acc[g], x[q], TA);
                         else mac_step(acc[g], x[q], TA);
                     }

@@ -44,6 +44,12 @@ struct MatArgs {
                                  // (natural); ~0u = all of a stripe's blocks (set at launch)
     uint32_t desc0;              // stripe_desc == nullptr: every stripe's {pattern << 8 |
                                  // outputs} word (0: pattern 0 with all m rows, the encode)
+    // Small reconstructs (at most kInlineDesc descriptors): the descriptors
+    // ride in the kernel arguments (stripe_desc == nullptr, n_inline > 0) --
+    // no upload of a descriptor array ahead of the kernel.
+    static constexpr int kInlineDesc = 16;
+    uint32_t n_inline;
+    uint2 inl_desc[kInlineDesc];
 };
 
 // Fills in chunks/groups/iters from k, m, ncols16 and launches the kernel

@@ -277,6 +277,8 @@ struct rs_ctx {
     uint32_t xcd_split_enc = 0;  // ... split-table encode: blocks per region (0: natural order; RSMI_XCD_ENC_REGION)
     uint32_t xcd_split_rec = ~0u;  // ... split-table reconstruct: blocks per region (~0u: a stripe; RSMI_XCD_REC_REGION)
     std::string rec_name;        // rs_kernel_name(ctx, 1) when bitslice_rec
+    bool inline_desc = true;     // small reconstructs: descriptors in the kernel arguments
+    size_t small_split = 16;     // bit-sliced codes: calls of at most this many erased stripes use the split table
 
     // Immutable after rs_new: encode pattern (PatBlob layout, one pattern)
     // and enc [n][k] | gf exp [512] | gf log [256] | 2 KiB zero page.
@@ -781,8 +783,17 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     // 1..T to the smallest row-subset variant covering every parity row the
     // pattern uses (bitslice.hpp rec_tops: fewer accumulators, more waves per
     // SIMD), T + 1 to the full kernel.
-    const int split_e = use_bitslice_rec(c) ? c->bitslice_rec_min_e : (c->m + 1);
-    const int T = use_bitslice_rec(c) ? c->n_tops : 0;
+    // A small call (at most c->small_split erased stripes) goes to the
+    // split-table kernel whole: its blocks load 8 survivors at a time where
+    // the syndrome kernel walks 4 ahead through k + m input slots, so one
+    // stripe reconstructs in 0.041 ms instead of 0.048 (RS(64,16), 64 KiB,
+    // profiles/r05c/lat_*.json); past ~16 stripes its VALU cost loses.
+    size_t erased_stripes = 0;
+    if (use_bitslice_rec(c) && c->small_split > 0)
+        for (size_t i = 0; i < stripes && erased_stripes <= c->small_split; ++i) erased_stripes += c->h_cnt[pid[i]] != 0;
+    const bool small_split = use_bitslice_rec(c) && erased_stripes <= c->small_split;
+    const int split_e = use_bitslice_rec(c) && !small_split ? c->bitslice_rec_min_e : (c->m + 1);
+    const int T = use_bitslice_rec(c) && !small_split ? c->n_tops : 0;
     const size_t nk = static_cast<size_t>(T) + 2;
     auto kernel_of = [&](uint32_t p) -> size_t {
         if (static_cast<int>(c->h_cnt[p]) < split_e) return 0;
@@ -811,14 +822,20 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         if (kk == 0) max_lo = std::max<int>(max_lo, static_cast<int>(c->h_cnt[p]));
     }
     // Descriptors, then (for the syndrome kernels) each descriptor's mask
-    // record, in one upload.
+    // record, in one upload -- or, for a small call, in the kernel arguments
+    // (no descriptor copy queued ahead of the kernel).
+    constexpr size_t kInline = rsmi::MatArgs::kInlineDesc;
+    static_assert(kInline == rsmi::BitsliceRecArgs::kInlineDesc, "inline descriptor counts differ");
+    const bool inl = used <= kInline && c->inline_desc;
     const bool masks = used > count[0];
     const size_t mask_off = round_up(used * sizeof(uint2), 16);
     const size_t desc_bytes = masks ? mask_off + used * sizeof(rsmi::BsStripeMask) : used * sizeof(uint2);
-    if (!L.st_stripe.acquire(desc_bytes)) return RS_ENOMEM;
-    uint2* desc = static_cast<uint2*>(L.st_stripe.p);
+    uint2 ldesc[kInline];
+    rsmi::BsStripeMask lmask[kInline];
+    if (!inl && !L.st_stripe.acquire(desc_bytes)) return RS_ENOMEM;
+    uint2* desc = inl ? ldesc : static_cast<uint2*>(L.st_stripe.p);
     rsmi::BsStripeMask* mrec =
-        reinterpret_cast<rsmi::BsStripeMask*>(static_cast<uint8_t*>(L.st_stripe.p) + mask_off);
+        inl ? lmask : reinterpret_cast<rsmi::BsStripeMask*>(static_cast<uint8_t*>(L.st_stripe.p) + mask_off);
     auto put = [&](size_t slot, size_t i) {
         const uint32_t p = pid[i];
         desc[slot] = make_uint2(static_cast<uint32_t>(i), (p << 8) | c->h_cnt[p]);
@@ -855,15 +872,22 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     }
     L.begin(s);  // the descriptor buffer's previous readers
     const bool waited = wait_patterns_for(c, L, max_pid, s);
-    if (!L.d_stripe_pat.reserve_on(desc_bytes, s)) return RS_ENOMEM;
-    hipError_t e = hipMemcpyAsync(L.d_stripe_pat.p, desc, desc_bytes, hipMemcpyHostToDevice, s);
-    L.st_stripe.release_after(s);
-    if (e != hipSuccess) return RS_EDEVICE;
-    const uint2* d_desc = static_cast<const uint2*>(L.d_stripe_pat.p);
+    hipError_t e = hipSuccess;
+    if (!inl) {
+        if (!L.d_stripe_pat.reserve_on(desc_bytes, s)) return RS_ENOMEM;
+        e = hipMemcpyAsync(L.d_stripe_pat.p, desc, desc_bytes, hipMemcpyHostToDevice, s);
+        L.st_stripe.release_after(s);
+        if (e != hipSuccess) return RS_EDEVICE;
+    }
+    const uint2* d_desc = inl ? nullptr : static_cast<const uint2*>(L.d_stripe_pat.p);
     if (count[0] > 0) {
         rsmi::MatArgs a = base_args(c, data, dss, parity, pss, pitch, len, count[0]);
         set_cache_patterns(c, a);
         a.stripe_desc = d_desc;
+        if (inl) {
+            a.n_inline = static_cast<uint32_t>(count[0]);
+            std::copy(ldesc, ldesc + count[0], a.inl_desc);
+        }
         a.shard_ptrs = shard_ptrs;
         e = rsmi::launch_matmul(a, max_lo, s);
     }
@@ -881,9 +905,14 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         b.parity_ss = a.parity_ss;
         b.pitch = a.pitch;
         b.count = a.stripes;
-        b.stripe_desc = d_desc + first;
-        b.stripe_mask = reinterpret_cast<const rsmi::BsStripeMask*>(static_cast<const uint8_t*>(L.d_stripe_pat.p) +
-                                                                    mask_off) + first;
+        if (inl) {
+            std::copy(ldesc + first, ldesc + first + count[kk], b.inl_desc);
+            std::copy(lmask + first, lmask + first + count[kk], b.inl_mask);
+        } else {
+            b.stripe_desc = d_desc + first;
+            b.stripe_mask = reinterpret_cast<const rsmi::BsStripeMask*>(
+                                static_cast<const uint8_t*>(L.d_stripe_pat.p) + mask_off) + first;
+        }
         b.coef = a.coef;
         b.src = a.src;
         b.dst = a.dst;
@@ -1562,6 +1591,13 @@ int rs_new_on_device(int k, int n, int device, rs_ctx** out) {
         if (qv) c->xcd_split_rec = static_cast<uint32_t>(std::min(std::max(0, std::atoi(qv)), 1 << 20));
         const char* bv = std::getenv("RSMI_XCD_BS_STRIPES");  // A/B knob: stripes per region (bit-sliced)
         if (bv && c->xcd) c->xcd = static_cast<uint32_t>(std::min(std::max(1, std::atoi(bv)), 64));
+    }
+    // Small reconstructs pass their descriptors in the kernel arguments
+    // (launch_reconstruct); RSMI_NO_INLINE_DESC=1 uploads them always (A/B, tests).
+    c->inline_desc = std::getenv("RSMI_NO_INLINE_DESC") == nullptr;
+    {
+        const char* ss = std::getenv("RSMI_SMALL_SPLIT");  // 0: never (A/B, tests)
+        if (ss) c->small_split = static_cast<size_t>(std::max(0, std::atoi(ss)));
     }
     {
         // Pattern-cache bound (RSMI_PATTERN_CAP, for tests): 2^20 patterns,

@@ -126,10 +126,15 @@ Status FEC::DecodeShared(std::vector<uint8_t>* dst, const std::vector<std::share
         nums[i] = shares[i]->Number;
         ptrs[i] = shares[i]->Data.data();
     }
-    std::vector<uint8_t> out(static_cast<size_t>(k_) * S);
-    const int rc = rs_decode(ctx_, nums.data(), ptrs.data(), cnt, S, out.data());
-    if (rc != RS_OK) return from(rc, "Decode");
-    *dst = std::move(out);
+    // Decoded straight into the caller's vector: a caller that reuses it
+    // (a receive loop's ReceiveEvent) reuses its capacity -- no fresh 1 MiB
+    // allocation and zero-fill per message.
+    dst->resize(static_cast<size_t>(k_) * S);
+    const int rc = rs_decode(ctx_, nums.data(), ptrs.data(), cnt, S, dst->data());
+    if (rc != RS_OK) {
+        dst->clear();
+        return from(rc, "Decode");
+    }
     return Status::Ok();
 }
 

@@ -15,7 +15,8 @@
 //                      (k+1)-th Receive that decodes the pool (main.go:52-107); Shards
 //                      handed over (Receive(Shard&&): the pool keeps their bytes)
 //   receive_copy_then_decode  the same through Receive(const Shard&) (each pooled
-//                      share copied)
+//                      share copied); *_pool10 / *_trigger split either into the k
+//                      pooling calls and the decoding arrival
 //   memcpy_wire        one memcpy of the n shares' bytes (the "one marshal copy" yardstick)
 // No signer / verifier (ed25519 is out of scope); the hash policy is off.
 #include "plugin_latency.hpp"
@@ -151,24 +152,35 @@ Status PluginLatency(const std::vector<uint8_t>& blob, int k, int n, const std::
         }
         return msgs;
     };
+    // One ReceiveEvent for the whole loop, as a receive loop would keep one:
+    // the decode reuses its message buffer.
     for (int variant = 0; variant < 2; ++variant) {
         std::unique_ptr<ShardPlugin> rp = NewShardPlugin(nullptr, nullptr, k, n);
-        std::vector<double> t;
+        std::vector<double> t, tpool, ttrig;
         bool ok = true;
+        ReceiveEvent ev;
         for (int r = 0; r < reps + 2; ++r) {
             std::vector<Shard> msgs = make_msgs(variant * 100000 + r);
-            ReceiveEvent ev;
             const auto t0 = std::chrono::steady_clock::now();
-            for (Shard& s : msgs) {
-                st = variant == 0 ? rp->Receive(self, std::move(s), &ev) : rp->Receive(self, s, &ev);
+            auto t1 = t0;
+            for (size_t i = 0; i < msgs.size(); ++i) {
+                if (i + 1 == msgs.size()) t1 = std::chrono::steady_clock::now();
+                st = variant == 0 ? rp->Receive(self, std::move(msgs[i]), &ev) : rp->Receive(self, msgs[i], &ev);
                 if (!st.ok()) break;
             }
-            const auto t1 = std::chrono::steady_clock::now();
+            const auto t2 = std::chrono::steady_clock::now();
             ok &= st.ok() && ev.decoded && ev.decode_status.ok() && ev.message == blob;
-            if (r >= 2) t.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            if (r >= 2) {
+                t.push_back(std::chrono::duration<double, std::milli>(t2 - t0).count());
+                tpool.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+                ttrig.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+            }
         }
         if (!ok) return Status::Err(RS_EINVAL, "PluginLatency: Receive did not decode the blob");
-        (*out)[variant == 0 ? "receive_then_decode" : "receive_copy_then_decode"] = median(t);
+        const std::string tag = variant == 0 ? "receive" : "receive_copy";
+        (*out)[tag + "_then_decode"] = median(t);
+        (*out)[tag + "_pool10"] = median(tpool);
+        (*out)[tag + "_trigger"] = median(ttrig);
     }
     (*out)["wire_bytes"] = static_cast<double>(wire_bytes);
     (*out)["sink"] = sink;  // keeps the broadcast callback's reads

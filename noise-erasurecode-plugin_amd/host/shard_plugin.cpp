@@ -288,7 +288,11 @@ Status ShardPlugin::Receive(const PeerID& sender, Shard&& msg, ReceiveEvent* ev)
 Status ShardPlugin::receive(const PeerID& sender, const Shard& msg, std::vector<uint8_t>* take, ReceiveEvent* ev) {
     ReceiveEvent local;
     ReceiveEvent& e = ev ? *ev : local;
-    e = ReceiveEvent{};
+    // Reset, keeping e.message's capacity for the decode (a caller that
+    // reuses its event decodes into the same buffer every time).
+    e.pooled = e.decoded = e.verified = false;
+    e.decode_status = Status::Ok();
+    e.message.clear();
     const std::string key = HexString(msg.FileSignature);
     std::vector<PoolEntry> pool;
     PoolEntry mine;  // this shard as a pool entry, built outside the lock

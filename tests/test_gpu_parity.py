@@ -313,6 +313,58 @@ def test_bitslice_reconstruct_roundtrip(k, n, S, pitch):
     ft.close()
 
 
+_DIAG_CHILD = r"""
+import sys
+import numpy as np
+import torch
+root = sys.argv[1]
+sys.path[:0] = [root, root + "/noise-erasurecode-plugin_amd"]
+import rsmi
+er = np.load(sys.argv[2])
+k, n, S = 64, 80, 65536
+m = n - k
+f = rsmi.FEC(k, n)
+assert f.kernel_name(1).startswith("bitslice_rec"), f.kernel_name(1)
+stripes = len(er)
+data = torch.empty(stripes * k * S, dtype=torch.uint8, device="cuda")
+parity = torch.empty(stripes * m * S, dtype=torch.uint8, device="cuda")
+f.fill_splitmix(data.data_ptr(), data.numel(), 99)
+f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+f.sync()
+d0, p0 = data.clone(), parity.clone()
+data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0
+parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0
+f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+f.sync()
+assert torch.equal(data, d0) and torch.equal(parity, p0)
+print("DIAG_DONE", flush=True)
+"""
+
+
+def test_mask_diagnostic_build(tmp_path):
+    """the syndrome kernel clamps a parity survivor's slot
+    (gen_bitslice.cpp) so that a wrong host mask record could only give wrong
+    bytes, never a fault.  lib_diag/ (the Makefile's gen_bitslice -M build)
+    re-derives every stripe's masks on the GPU from the pattern's id rows and
+    prints RSMI_MASK_MISMATCH / RSMI_MASK_SLOT_OVERFLOW on any disagreement.
+    Run it over the straddling edge sets and a fresh config-5 mix (1-16
+    erasures, 512 stripes of 64 KiB): no report, and the round trip holds."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "noise-erasurecode-plugin_amd", "lib_diag", "librsmi.so")
+    assert os.path.exists(lib), "lib_diag/librsmi.so is built by the Makefile (build())"
+    k, n = 64, 80
+    er = np.concatenate([_fixed_patterns(k, n), _erasures(np.random.default_rng(16), 512, n, n - k)])
+    np.save(tmp_path / "er.npy", er)
+    env = dict(os.environ, RSMI_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", _DIAG_CHILD, root, str(tmp_path / "er.npy")], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "DIAG_DONE" in r.stdout, r.stdout[-2000:]
+    assert "RSMI_MASK_" not in r.stdout, r.stdout[-2000:]
+
+
 def _lowest_parity_row(er_row, k, n):
     """Python restatement of rsmi.cpp lowest_parity_row: the lowest parity
     row a pattern uses (erased parity outputs and Rebuild's parity
@@ -393,8 +445,9 @@ def _check_ptrs_roundtrip(f, k, n, S, er, seed):
     assert torch.equal(pool[rows.view(-1), :S].view(stripes, n, S), full)
 
 
+@pytest.mark.parametrize("small_split", ["0", "16"])
 @pytest.mark.parametrize("k,n", [(8, 14), (64, 80)])
-def test_bitslice_rec_past_2gib(k, n):
+def test_bitslice_rec_past_2gib(k, n, small_split):
     """the syndrome kernel's buffer loads gave a present
     input a 0x7FFFFFFF-byte range, so every column at or past 2 GiB read as
     zeros while rs_reconstruct_* accept shards up to 2^28 columns.  One
@@ -403,8 +456,10 @@ def test_bitslice_rec_past_2gib(k, n):
     survivor, one allocation), data shards 1 and 5 erased.  The outputs at
     sampled columns on both sides of 2 GiB and at the ragged end equal the
     oracle's Rebuild of the same k survivors at those columns (Rebuild is
-    column-wise linear, so any bytes will do, codeword or not)."""
-    f = fec(k, n)
+    column-wise linear, so any bytes will do, codeword or not).  small_split
+    "0" keeps the one-stripe call on the syndrome kernel (the one the range
+    bug was in); "16" (the default) sends it to the split-table kernel."""
+    f = _fec_env(k, n, RSMI_SMALL_SPLIT=small_split)
     assert f.kernel_name(1).startswith("bitslice_rec")
     m = n - k
     S = (1 << 31) + 8192 + 40
@@ -437,6 +492,7 @@ def test_bitslice_rec_past_2gib(k, n):
         # the ragged last column holds S % 16 = 8 real bytes; the rest is padding
         assert got[:L - 8] == want[:L - 8], (k, n, i)
     del X, outs
+    f.close()
 
 
 def test_reconstruct_split_between_kernels():
@@ -468,7 +524,7 @@ def test_bitslice_reconstruct_matches_oracle_rebuild():
     the oracle's Rebuild of the same survivors (byte for byte)."""
     k, n, S, stripes = 64, 80, 4096, 6
     m = n - k
-    f = fec(64, 80)
+    f = _fec_env(64, 80, RSMI_SMALL_SPLIT="0")  # 6 stripes: keep them on the syndrome kernel
     data, parity = _dev_stripes(f, stripes, S, S, 2024)
     f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
     f.sync()
@@ -1019,6 +1075,43 @@ def test_rs8_14_row_group_of_six(S, pitch):
         assert torch.equal(parity.view(stripes, m, pitch)[:, :, :S], p0.view(stripes, m, pitch)[:, :, :S])
 
 
+@pytest.mark.parametrize("k,n,env", [(10, 14, {}), (64, 80, {}), (64, 80, {"RSMI_SMALL_SPLIT": "0"}),
+                                     (64, 80, {"RSMI_BITSLICE_REC_MIN_E": "5", "RSMI_SMALL_SPLIT": "0"}),
+                                     (8, 14, {}), (8, 14, {"RSMI_SMALL_SPLIT": "0"})])
+@pytest.mark.parametrize("stripes", [1, 2, 15, 16, 17, 40])
+def test_inline_descriptor_threshold(k, n, env, stripes):
+    """a reconstruct of at most 16 erased stripes passes its
+    stripe descriptors (and mask records) in the kernel arguments instead of
+    uploading them; more stripes upload.  Both sides of the threshold, every
+    kernel (split table, syndrome, the two split between kernels in one
+    call; a bit-sliced code's small calls go to the split table unless
+    RSMI_SMALL_SPLIT=0), strided and pointer mode: the regenerated shards
+    equal the originals and the upload path's output (RSMI_NO_INLINE_DESC)."""
+    m = n - k
+    S = 4096 + 48
+    f_in = _fec_env(k, n, **env)
+    f_up = _fec_env(k, n, RSMI_NO_INLINE_DESC="1", **env)
+    rng = np.random.default_rng(stripes * 31 + k)
+    er = _erasures(rng, stripes, n, m)
+    if stripes > 2:
+        er[1] = 0  # a stripe with nothing erased is skipped (not a descriptor)
+    data, parity = _dev_stripes(f_in, stripes, S, S, 5 + stripes)
+    f_in.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
+    f_in.sync()
+    d0, p0 = data.clone(), parity.clone()
+    for f in (f_in, f_up):
+        data.copy_(d0)
+        parity.copy_(p0)
+        data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0xEE
+        parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0xEE
+        f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
+        f.sync()
+        assert torch.equal(data, d0) and torch.equal(parity, p0)
+    _check_ptrs_roundtrip(f_in, k, n, S, er, 9 + stripes)
+    f_in.close()
+    f_up.close()
+
+
 @pytest.mark.parametrize("k,n", [(10, 14), (64, 80), (200, 256)])
 def test_erasure_flags_any_nonzero_byte(k, n):
     """rs_reconstruct_stripes treats any non-zero flag byte as erased (the
@@ -1091,8 +1184,9 @@ def test_xcd_block_order_matches_natural(k, n, S, stripes):
     forced on every kernel (RSMI_XCD=1) and with a region of 3 blocks for
     the split-table encode."""
     m = n - k
-    fx = {"0": _fec_env(k, n, RSMI_XCD="0"), "1": _fec_env(k, n, RSMI_XCD="1"),
-          "r3": _fec_env(k, n, RSMI_XCD_ENC_REGION="3")}
+    # RSMI_SMALL_SPLIT=0: small calls stay on the bit-sliced kernels (whose block order is under test)
+    fx = {"0": _fec_env(k, n, RSMI_XCD="0", RSMI_SMALL_SPLIT="0"), "1": _fec_env(k, n, RSMI_XCD="1", RSMI_SMALL_SPLIT="0"),
+          "r3": _fec_env(k, n, RSMI_XCD_ENC_REGION="3", RSMI_SMALL_SPLIT="0")}
     rng = np.random.default_rng(stripes * 31 + k)
     er = _erasures(rng, stripes, n, m)
     data, parity = _dev_stripes(fx["0"], stripes, S, S, 5 + stripes)
