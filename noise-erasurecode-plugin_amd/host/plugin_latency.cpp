@@ -154,12 +154,16 @@ Status PluginLatency(const std::vector<uint8_t>& blob, int k, int n, const std::
     };
     // One ReceiveEvent for the whole loop, as a receive loop would keep one:
     // the decode reuses its message buffer.
+    // A fresh plugin per rep (outside the timed region): without a verifier
+    // nothing deletes a decoded pool, and pools kept across reps would make
+    // every pooled copy land on never-touched heap pages (page faults the
+    // steady state of a verifying receiver does not pay).
     for (int variant = 0; variant < 2; ++variant) {
-        std::unique_ptr<ShardPlugin> rp = NewShardPlugin(nullptr, nullptr, k, n);
         std::vector<double> t, tpool, ttrig;
         bool ok = true;
         ReceiveEvent ev;
         for (int r = 0; r < reps + 2; ++r) {
+            std::unique_ptr<ShardPlugin> rp = NewShardPlugin(nullptr, nullptr, k, n);
             std::vector<Shard> msgs = make_msgs(variant * 100000 + r);
             const auto t0 = std::chrono::steady_clock::now();
             auto t1 = t0;

@@ -127,11 +127,22 @@ def main():
                 counts[key] += v
 
     threads = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
+    # Process CPU time (every thread, user + system) over the soak: with the
+    # engine's polled waits (rsmi::wait_event, RSMI_SYNC_SPIN_US /
+    # RSMI_SYNC_SPINNERS / RSMI_SYNC_ADAPTIVE) against runs without polling,
+    # the difference is what the polling costs.
+    cpu0, wall0 = time.process_time(), time.time()
     for t in threads:
         t.start()
     for t in threads:
         t.join()
+    cpu, wall = time.process_time() - cpu0, time.time() - wall0
+    ncalls = sum(counts.values())
     print(json.dumps({"code": a.code, "shard": a.shard, "seconds": a.seconds, "threads": a.threads, "calls": counts,
+                      "cpu_seconds": round(cpu, 2), "cpu_cores_busy": round(cpu / wall, 2),
+                      "cpu_ms_per_call": round(1e3 * cpu / max(1, ncalls), 4),
+                      "spin_env": {v: os.environ.get(v) for v in ("RSMI_SYNC_SPIN_US", "RSMI_SYNC_SPINNERS",
+                                                                  "RSMI_SYNC_ADAPTIVE")},
                       "pattern_cap": os.environ.get("RSMI_PATTERN_CAP"), "evictions": f.pattern_evictions(),
                       "patterns": f.pattern_count(), "leases": f.stat(f.STAT_LEASES),
                       "failures": len(failures), "first_failures": failures[:5]}))
