@@ -176,6 +176,8 @@ enum {
     RS_STAT_LEASES = 4,            /* leases created (peak concurrent calls)          */
     RS_STAT_ENCODES_IN_PLACE = 5,  /* rs_encode calls served from engine-pinned memory */
     RS_STAT_DECODES_IN_PLACE = 6,  /* rs_decode calls that read engine-pinned survivors in place */
+    RS_STAT_REC_STRIPES_TABLE = 7,  /* stripes reconstructed by the split-table kernel (batched API) */
+    RS_STAT_REC_STRIPES_SYNDROME = 8, /* ... by the bit-sliced syndrome kernels                     */
 };
 int64_t rs_stat(const rs_ctx *ctx, int which);
 

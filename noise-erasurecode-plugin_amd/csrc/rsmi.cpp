@@ -309,6 +309,7 @@ struct rs_ctx {
     std::atomic<int64_t> batches_in_place{0}, batches_staged{0};  // rs_decode_batch paths (rs_stat)
     std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
     std::atomic<int64_t> decodes_in_place{0};                     // rs_decode from engine-pinned memory
+    std::atomic<int64_t> rec_stripes_table{0}, rec_stripes_syndrome{0};  // launch_reconstruct's kernels (rs_stat)
     hipEvent_t pat_ev = nullptr;
     hipStream_t build_stream = nullptr;  // pattern builds (flush_patterns), off every caller's stream
     hipEvent_t caller_ev = nullptr;      // the building caller's stream tail (build_after_caller)
@@ -783,15 +784,15 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
     // 1..T to the smallest row-subset variant covering every parity row the
     // pattern uses (bitslice.hpp rec_tops: fewer accumulators, more waves per
     // SIMD), T + 1 to the full kernel.
-    // A small call (at most c->small_split erased stripes) goes to the
-    // split-table kernel whole: its blocks load 8 survivors at a time where
-    // the syndrome kernel walks 4 ahead through k + m input slots, so one
-    // stripe reconstructs in 0.041 ms instead of 0.048 (RS(64,16), 64 KiB,
-    // profiles/r05c/lat_*.json); past ~16 stripes its VALU cost loses.
+    // A small call (at most c->small_split erased stripes; 0: never) goes to
+    // the split-table kernel whole: its blocks load 8 survivors at a time
+    // where the syndrome kernel walks 4 ahead through k + m input slots, so
+    // one RS(64,16) 64 KiB stripe reconstructs in 0.0375 ms instead of 0.048
+    // (profiles/r05c/, r05d/lat_*.json); past ~16 stripes its VALU cost loses.
     size_t erased_stripes = 0;
     if (use_bitslice_rec(c) && c->small_split > 0)
         for (size_t i = 0; i < stripes && erased_stripes <= c->small_split; ++i) erased_stripes += c->h_cnt[pid[i]] != 0;
-    const bool small_split = use_bitslice_rec(c) && erased_stripes <= c->small_split;
+    const bool small_split = use_bitslice_rec(c) && c->small_split > 0 && erased_stripes <= c->small_split;
     const int split_e = use_bitslice_rec(c) && !small_split ? c->bitslice_rec_min_e : (c->m + 1);
     const int T = use_bitslice_rec(c) && !small_split ? c->n_tops : 0;
     const size_t nk = static_cast<size_t>(T) + 2;
@@ -927,6 +928,10 @@ int launch_reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity
         e = kk <= static_cast<size_t>(T) ? c->bitslice->rec_top_launch[kk - 1](b, s) : c->bitslice->reconstruct(b, s);
     }
     L.end(s);  // under pat_mu: an eviction waits for these launches
+    if (e == hipSuccess) {
+        c->rec_stripes_table += static_cast<int64_t>(count[0]);
+        c->rec_stripes_syndrome += static_cast<int64_t>(used - count[0]);
+    }
     if (waited && e == hipSuccess) seen_patterns(c, L);
     return hip_status(e);
 }
@@ -1717,6 +1722,8 @@ int64_t rs_stat(const rs_ctx* c, int which) {
         case RS_STAT_BATCHES_STAGED: return c->batches_staged.load();
         case RS_STAT_ENCODES_IN_PLACE: return c->encodes_in_place.load();
         case RS_STAT_DECODES_IN_PLACE: return c->decodes_in_place.load();
+        case RS_STAT_REC_STRIPES_TABLE: return c->rec_stripes_table.load();
+        case RS_STAT_REC_STRIPES_SYNDROME: return c->rec_stripes_syndrome.load();
         case RS_STAT_LEASES: {
             std::lock_guard<std::mutex> lk(const_cast<rs_ctx*>(c)->lease_mu);
             return static_cast<int64_t>(c->leases.size());

@@ -305,7 +305,7 @@ class FEC:
         return _lib().rs_pattern_count(self._h)
 
     (STAT_PATTERNS, STAT_EVICTIONS, STAT_BATCHES_IN_PLACE, STAT_BATCHES_STAGED, STAT_LEASES,
-     STAT_ENCODES_IN_PLACE, STAT_DECODES_IN_PLACE) = range(7)
+     STAT_ENCODES_IN_PLACE, STAT_DECODES_IN_PLACE, STAT_REC_STRIPES_TABLE, STAT_REC_STRIPES_SYNDROME) = range(9)
 
     def stat(self, which: int) -> int:
         return _lib().rs_stat(self._h, which)

@@ -474,8 +474,10 @@ def test_bitslice_rec_past_2gib(k, n, small_split):
     tab = torch.tensor(table, dtype=torch.int64, device="cuda")
     er = np.zeros((1, n), dtype=np.uint8)
     er[0, erased] = 1
+    syn0 = f.stat(f.STAT_REC_STRIPES_SYNDROME)
     f.reconstruct_ptrs(tab.data_ptr(), S, 1, er.tobytes())
     f.sync()
+    assert f.stat(f.STAT_REC_STRIPES_SYNDROME) - syn0 == (1 if small_split == "0" else 0)  # the kernel under test ran
     c2g = 1 << 27  # the column at 2 GiB
     cols = [0, 1, 511, 512, c2g - 513, c2g - 1, c2g, c2g + 1, c2g + 511, c2g + 512, Sp // 16 - 2, Sp // 16 - 1]
     idx = torch.tensor([16 * c + b for c in cols for b in range(16)], dtype=torch.int64, device="cuda")
@@ -525,6 +527,7 @@ def test_bitslice_reconstruct_matches_oracle_rebuild():
     k, n, S, stripes = 64, 80, 4096, 6
     m = n - k
     f = _fec_env(64, 80, RSMI_SMALL_SPLIT="0")  # 6 stripes: keep them on the syndrome kernel
+    assert f.stat(f.STAT_REC_STRIPES_SYNDROME) == 0
     data, parity = _dev_stripes(f, stripes, S, S, 2024)
     f.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
     f.sync()
@@ -544,6 +547,7 @@ def test_bitslice_reconstruct_matches_oracle_rebuild():
         rc, ref = oracle.decode(E, k, n, [(i, sh[i]) for i in keep[:k]])
         assert rc == 0 and ref == got[s].tobytes(), s
     assert parity.cpu().numpy().reshape(stripes, m, S).tobytes() == hp.tobytes()
+    assert f.stat(f.STAT_REC_STRIPES_SYNDROME) == stripes
 
 
 def test_fill_splitmix_matches_oracle():
@@ -1099,14 +1103,24 @@ def test_inline_descriptor_threshold(k, n, env, stripes):
     f_in.encode_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes)
     f_in.sync()
     d0, p0 = data.clone(), parity.clone()
+    erased = int((er.sum(axis=1) > 0).sum())
+    bitsliced = f_in.kernel_name(1).startswith("bitslice_rec")
+    small = env.get("RSMI_SMALL_SPLIT", "16") != "0" and erased <= 16
     for f in (f_in, f_up):
         data.copy_(d0)
         parity.copy_(p0)
         data.view(stripes, k, S)[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0xEE
         parity.view(stripes, m, S)[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0xEE
+        t0, s0 = f.stat(f.STAT_REC_STRIPES_TABLE), f.stat(f.STAT_REC_STRIPES_SYNDROME)
         f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
         f.sync()
         assert torch.equal(data, d0) and torch.equal(parity, p0)
+        dt, ds = f.stat(f.STAT_REC_STRIPES_TABLE) - t0, f.stat(f.STAT_REC_STRIPES_SYNDROME) - s0
+        assert dt + ds == erased
+        if not bitsliced or small:
+            assert ds == 0, (dt, ds)  # the split-table kernel took every stripe
+        elif "RSMI_BITSLICE_REC_MIN_E" not in env:
+            assert dt == 0, (dt, ds)  # the syndrome kernel took every stripe
     _check_ptrs_roundtrip(f_in, k, n, S, er, 9 + stripes)
     f_in.close()
     f_up.close()
@@ -1205,9 +1219,12 @@ def test_xcd_block_order_matches_natural(k, n, S, stripes):
         dv, pv = data.view(stripes, k, S), parity.view(stripes, m, S)
         dv[torch.from_numpy(er[:, :k].astype(bool)).cuda()] = 0xA5
         pv[torch.from_numpy(er[:, k:].astype(bool)).cuda()] = 0x5A
+        s0 = f.stat(f.STAT_REC_STRIPES_SYNDROME)
         f.reconstruct_stripes(data.data_ptr(), k * S, parity.data_ptr(), m * S, S, S, stripes, er.tobytes())
         f.sync()
         assert torch.equal(data, d0) and torch.equal(parity, p0), name
+        if f.kernel_name(1).startswith("bitslice_rec"):
+            assert f.stat(f.STAT_REC_STRIPES_SYNDROME) - s0 == int((er.sum(axis=1) > 0).sum()), name
     for f in fx.values():
         f.close()
 

@@ -38,9 +38,14 @@ def main():
     while time.time() - t0 < a.seconds:
         k, n = codes[int(rng.integers(0, len(codes)))]
         m = n - k
-        if (k, n) not in fecs:
-            fecs[(k, n)] = rsmi.NewFEC(k, n)
-        f = fecs[(k, n)]
+        # half the contexts keep small calls on the bit-sliced kernels
+        # (RSMI_SMALL_SPLIT=0), half route them to the split table (default)
+        small = "0" if rng.integers(0, 2) else "16"
+        if (k, n, small) not in fecs:
+            os.environ["RSMI_SMALL_SPLIT"] = small
+            fecs[(k, n, small)] = rsmi.NewFEC(k, n)
+            del os.environ["RSMI_SMALL_SPLIT"]
+        f = fecs[(k, n, small)]
         S = int(rng.choice([1, 15, 16, 100, 4096, 8192 + 16, 65536, 70000, 1 << 20]))
         if k * S > (64 << 20):
             S = max(1, (64 << 20) // k)
