@@ -207,10 +207,11 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
             for (int j = 0; j < K; ++j) sp[j] = uniform_ptr(reinterpret_cast<uint8_t*>(tp[ids[j]]));
         } else {
             uint8_t* dbase = a.data + s * a.data_ss;
-            uint8_t* pbase = a.parity + s * a.parity_ss - static_cast<uint64_t>(K) * a.pitch;
+            uint8_t* pbase = a.parity + s * a.parity_ss;
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                sp[j] = (ids[j] < static_cast<uint32_t>(K) ? dbase : pbase) + static_cast<uint64_t>(ids[j]) * a.pitch;
+                sp[j] = ids[j] < static_cast<uint32_t>(K) ? dbase + static_cast<uint64_t>(ids[j]) * a.pitch
+                                                         : pbase + static_cast<uint64_t>(ids[j] - K) * a.pitch;
         }
     } else {
         for (int i = threadIdx.x; i < k; i += BT) sptr[i] = shard(srcid ? srcid[i] : static_cast<uint32_t>(i));
@@ -251,10 +252,11 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
             for (int r = 0; r < TG * 4; ++r) dp[r] = uniform_ptr(reinterpret_cast<uint8_t*>(tp[oid[r]]));
         } else {
             uint8_t* dbase = a.data + s * a.data_ss;
-            uint8_t* pbase = a.parity + s * a.parity_ss - static_cast<uint64_t>(a.k) * a.pitch;
+            uint8_t* pbase = a.parity + s * a.parity_ss;
 #pragma unroll
             for (int r = 0; r < TG * 4; ++r)
-                dp[r] = (oid[r] < a.k ? dbase : pbase) + static_cast<uint64_t>(oid[r]) * a.pitch;
+                dp[r] = oid[r] < a.k ? dbase + static_cast<uint64_t>(oid[r]) * a.pitch
+                                     : pbase + static_cast<uint64_t>(oid[r] - a.k) * a.pitch;
         }
     }
     // Split tables of rows [row0, row0 + MG): sub-step (j, g) holds rows

@@ -119,7 +119,8 @@ public:
     // into one reused wire buffer: each share byte is copied once, where the
     // reference copies it twice (DeepCopy main.go:255-258, then Marshal).
     // broadcast gets each message's wire bytes, valid during the call; calls
-    // on one plugin serialise on the buffers.
+    // on one plugin serialise on the buffers, so broadcast must not call
+    // ShardAndBroadcastWire on the same plugin (Receive is fine).
     Status ShardAndBroadcastWire(const PeerID& self, const std::vector<uint8_t>* input,
                                  const std::function<void(const uint8_t* wire, size_t len)>& broadcast);
     // main.go:211-241 (input == nullptr -> "network: input is null").
