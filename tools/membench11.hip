@@ -16,6 +16,8 @@
 //   writes      the 4 stores only
 //   batch<B>    grid-stride over the pieces, B pieces per block per batch: B x 10
 //               loads, then B x 4 stores (per-block bursts, no clock)
+//   plain phased  plain, its loads started inside a read window of a clock period P
+//               and its stores inside the write window after it
 //   phased<B>   batch<B>, each batch's loads start inside a read window and its
 //               stores inside the following write window of a clock period P
 //               (read fraction f of P)
@@ -76,9 +78,24 @@ __device__ __forceinline__ void piece_store(const Args& a, uint32_t q, const u32
     for (int t = 0; t < M; ++t) st(a.par + (s * M + t) * PITCH + col, acc[t]);
 }
 
+__device__ __forceinline__ void wait_window(uint64_t pmask, uint64_t lo, uint64_t hi) {
+    for (;;) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime() & pmask;
+        if (t >= lo && t < hi) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 __global__ __launch_bounds__(256) void plain(Args a) {
     const uint32_t q = blockIdx.x;
     u32x4 acc[M];
+    if (a.mode == 3) {  // the encode's shape, loads in a read window, stores in a write window
+        wait_window(a.pmask, 0, a.rwin);
+        piece_io(a, q, acc);
+        wait_window(a.pmask, a.rwin, a.pmask + 1);
+        piece_store(a, q, acc);
+        return;
+    }
     if (a.mode == 2) {
 #pragma unroll
         for (int t = 0; t < M; ++t) acc[t] = u32x4{q, 1u, 2u, (unsigned)t};
@@ -93,12 +110,8 @@ __global__ __launch_bounds__(256) void plain(Args a) {
     piece_store(a, q, acc);
 }
 
-__device__ __forceinline__ void wait_window(uint64_t pmask, uint64_t lo, uint64_t hi) {
-    for (;;) {
-        const uint64_t t = __builtin_amdgcn_s_memrealtime() & pmask;
-        if (t >= lo && t < hi) return;
-        __builtin_amdgcn_s_sleep(2);
-    }
+__global__ void clockprobe(uint64_t* t) {
+    if (threadIdx.x == 0) t[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <int B, bool kPhased>
@@ -145,12 +158,12 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     Args a{data, par, npieces, 0, 0, 0};
+    char name[128];
     auto run_plain = [&](uint32_t mode, double bytes, const char* name) {
         Args b = a;
         b.mode = mode;
         time([&] { hipLaunchKernelGGL(plain, dim3(npieces), dim3(256), 0, 0, b); }, bytes, name);
     };
-    char name[128];
     auto run_batched = [&](auto kern, int B, bool phased, uint64_t period, double frac) {
         int per_cu = 0;
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
@@ -164,17 +177,36 @@ int main(int argc, char** argv) {
             snprintf(name, sizeof name, "batch<%d> (%u blocks)", B, grid);
         time([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, b); }, enc_bytes, name);
     };
+    {  // is the constant clock one clock for the chip?  blocks go to XCDs round-robin
+        uint64_t* d_t;
+        CK(hipMalloc(&d_t, 64 * sizeof(uint64_t)));
+        hipLaunchKernelGGL(clockprobe, dim3(64), dim3(64), 0, 0, d_t);
+        std::vector<uint64_t> t(64);
+        CK(hipMemcpy(t.data(), d_t, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        uint64_t lo = t[0];
+        for (uint64_t v : t) lo = v < lo ? v : lo;
+        printf("clock probe (block start - earliest, ticks of 10 ns, block b on XCD b %% 8):");
+        for (int b = 0; b < 64; ++b) printf("%s%llu", b % 8 ? " " : "\n  ", (unsigned long long)(t[b] - lo));
+        printf("\n");
+        CK(hipFree(d_t));
+    }
     for (int rep = 0; rep < 2; ++rep) {
         run_plain(0, enc_bytes, "plain (encode shape)");
         run_plain(1, double(stripes) * K * S, "reads only (10 per stripe)");
         run_plain(2, double(stripes) * M * S, "writes only (4 per stripe)");
-        run_batched(batched<1, false>, 1, false, 0, 0);
+        for (uint64_t period : {32u, 64u, 128u, 256u, 512u})
+            for (double f : {0.6, 0.7, 0.8}) {
+                Args b = a;
+                b.mode = 3;
+                b.pmask = period - 1;
+                b.rwin = uint64_t(f * double(period));
+                snprintf(name, sizeof name, "plain phased P=%.2fus f=%.2f", period / 100.0, f);
+                time([&] { hipLaunchKernelGGL(plain, dim3(npieces), dim3(256), 0, 0, b); }, enc_bytes, name);
+            }
         run_batched(batched<2, false>, 2, false, 0, 0);
-        run_batched(batched<4, false>, 4, false, 0, 0);
-        for (uint64_t period : {256u, 1024u, 4096u, 16384u})
-            for (double f : {0.62, 0.72})
-                run_batched(batched<2, true>, 2, true, period, f);
-        for (uint64_t period : {1024u, 4096u, 16384u}) run_batched(batched<4, true>, 4, true, period, 0.68);
+        for (uint64_t period : {256u, 2048u})
+            run_batched(batched<2, true>, 2, true, period, 0.7);
+        run_batched(batched<4, true>, 4, true, 2048u, 0.7);
     }
     return 0;
 }
