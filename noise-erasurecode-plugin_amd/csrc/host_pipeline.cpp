@@ -6,6 +6,9 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#if defined(__x86_64__)
+#include <emmintrin.h>
+#endif
 
 namespace rsmi {
 
@@ -36,6 +39,52 @@ inline void cpu_relax() {
 #endif
 }
 }  // namespace
+
+namespace {
+bool stage_nt() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSMI_STAGE_NT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+}  // namespace
+
+void stage_copy(void* dst, const void* src, size_t n) {
+#if defined(__x86_64__)
+    if (stage_nt() && n >= 4096) {
+        uint8_t* d = static_cast<uint8_t*>(dst);
+        const uint8_t* s = static_cast<const uint8_t*>(src);
+        const size_t head = (16u - (reinterpret_cast<uintptr_t>(d) & 15u)) & 15u;
+        std::memcpy(d, s, head);
+        d += head;
+        s += head;
+        n -= head;
+        size_t i = 0;
+        for (; i + 64 <= n; i += 64) {
+            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
+            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 16));
+            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 32));
+            const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 48));
+            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16), b);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 32), c);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 48), e);
+        }
+        for (; i + 16 <= n; i += 16)
+            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i)));
+        std::memcpy(d + i, s + i, n - i);
+        return;
+    }
+#endif
+    std::memcpy(dst, src, n);
+}
+
+void stage_fence() {
+#if defined(__x86_64__)
+    if (stage_nt()) _mm_sfence();
+#endif
+}
 
 // Polled completion, bounded: a thread polls only while its
 // previous wait was short (at most the spin window: single-message calls),

@@ -78,6 +78,15 @@ private:
 // wake-up was a fixed ~10 us of the host API's latency.
 hipError_t wait_event(hipEvent_t ev);
 
+// Copies caller bytes into pinned staging that a kernel is about to read over
+// PCIe.  Non-temporal stores (then a store fence) leave the lines in DRAM
+// rather than dirty in the CPU's caches, where every GPU read would have to
+// snoop them out: one config-1 message's kernel reads its 1 MiB 4.7 us faster
+// (tools/stream_probe.hip, profiles/r05j/).  RSMI_STAGE_NT=0: plain memcpy.
+void stage_copy(void* dst, const void* src, size_t n);
+// The fence after a run of stage_copy calls (before the launch that reads them).
+void stage_fence();
+
 // Launches the GF kernel for one chunk: survivors at din + j*pitch (j < k),
 // outputs at dout + t*pitch, w coded bytes per shard.
 using ChunkLaunch = std::function<hipError_t(uint8_t* din, uint8_t* dout, size_t pitch,

@@ -1144,7 +1144,8 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     for (int j = 0; j < k; ++j) dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
     // survivors' columns [off, off + w) into staging, chunk by chunk
     auto stage = [&](size_t off, size_t w) {
-        for (int j = 0; j < k; ++j) std::memcpy(st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w);
+        for (int j = 0; j < k; ++j) rsmi::stage_copy(st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w);
+        rsmi::stage_fence();
     };
     const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
                                 stage_chunks(static_cast<size_t>(k) * S), stage);
@@ -1265,7 +1266,8 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
     for (int ch = 0; ch < nch && e == hipSuccess; ++ch) {
         // chunk ch's columns of every data shard into staging, then its launch
         const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
-        for (size_t j = 0; j < k; ++j) std::memcpy(st + j * span + off, input + j * S + off, w);
+        for (size_t j = 0; j < k; ++j) rsmi::stage_copy(st + j * span + off, input + j * S + off, w);
+        rsmi::stage_fence();
         rsmi::MatArgs a = base_args(c, static_cast<uint8_t*>(din) + off, 0, static_cast<uint8_t*>(dout) + off, 0, span, w, 1);
         set_patterns(c, 1, c->d_encpat.p, a);
         a.stripe_desc = nullptr;
