@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--erase", default=None,
                     help="fixed erased shard ids for every stripe, e.g. 0,1,2,3 (default random)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="budget of the CPU baseline sample (0 disables)")
+                    help="budget of the CPU baseline sample, timed on rank 0 at N = 1 only (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU this job may use (affinity and cgroup quota)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -691,7 +691,7 @@ def main():
     out = None
     if rank == 0:
         cpu = None
-        if args.cpu_seconds > 0:  # after the timed region, on rank 0, at every N
+        if args.cpu_seconds > 0 and world == 1:  # after the timed region, rank 0 at N = 1 only
             cpu = cpu_baseline(k, n, S, args.cpu_seconds, args.cpu_threads)
         out = {
             "metric": "RS(10,4) encode+reconstruct GB/s at 1/8 GPUs; % HBM roofline",
