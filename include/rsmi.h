@@ -120,6 +120,18 @@ int rs_decode(rs_ctx *ctx, int *numbers, const uint8_t **shares, int count,
 int rs_decode_batch(rs_ctx *ctx, int batch, const int *counts, int *numbers,
                     const uint8_t **shares, size_t share_len, uint8_t **dsts, int *status);
 
+/* rs_encode_batch: send-side batching, the counterpart of rs_decode_batch --
+ * Encode (main.go:262, once per message in shardInput main.go:243-267) for
+ * `batch` messages of this code in one GPU pass.  inputs[b] holds len bytes
+ * (len % k == 0, else every status is RS_ELEN_NOT_MULTIPLE); parities[b]
+ * receives (n - k) * len / k bytes laid out as rs_encode's parity.  The
+ * messages are staged through pinned memory in chunks (the staging copy of
+ * one chunk overlaps the kernel of the previous one, which reads and writes
+ * the staging over PCIe).  status[b] gets each message's code; returns RS_OK
+ * if every message encoded, else the first failing status. */
+int rs_encode_batch(rs_ctx *ctx, int batch, const uint8_t *const *inputs, size_t len,
+                    uint8_t *const *parities, int *status);
+
 /* ---- device-resident batched API (many stripes per launch) ---------------
  * Stripe s, shard i lives at
  *     i <  k:  data   + s * data_stripe_stride   + i       * shard_pitch
@@ -178,6 +190,7 @@ enum {
     RS_STAT_DECODES_IN_PLACE = 6,  /* rs_decode calls that read engine-pinned survivors in place */
     RS_STAT_REC_STRIPES_TABLE = 7,  /* stripes reconstructed by the split-table kernel (batched API) */
     RS_STAT_REC_STRIPES_SYNDROME = 8, /* ... by the bit-sliced syndrome kernels                     */
+    RS_STAT_ENCODE_BATCHES = 9,    /* rs_encode_batch calls coded in batched GPU passes */
 };
 int64_t rs_stat(const rs_ctx *ctx, int which);
 

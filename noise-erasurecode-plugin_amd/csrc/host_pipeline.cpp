@@ -155,8 +155,25 @@ bool CopyPool::claim(Job* j, size_t* part) {
     return true;
 }
 
+namespace {
+// Copies pieces [b, e); non-temporal pieces are fenced before the copier
+// reports them done (another thread's launch reads them next).
+void copy_pieces(const CopyPool::Piece* b, const CopyPool::Piece* e) {
+    bool nt = false;
+    for (const CopyPool::Piece* p = b; p != e; ++p) {
+        if (p->nt) {
+            stage_copy(p->dst, p->src, p->len);
+            nt = true;
+        } else {
+            std::memcpy(p->dst, p->src, p->len);
+        }
+    }
+    if (nt) stage_fence();
+}
+}  // namespace
+
 void CopyPool::copy_part(const Job& j, size_t part) {
-    for (size_t i = j.bounds[part]; i < j.bounds[part + 1]; ++i) std::memcpy(j.pieces[i].dst, j.pieces[i].src, j.pieces[i].len);
+    copy_pieces(j.pieces.data() + j.bounds[part], j.pieces.data() + j.bounds[part + 1]);
 }
 
 void CopyPool::worker() {
@@ -195,7 +212,7 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
     size_t total = 0;
     for (const Piece& p : pieces) total += p.len;
     if (total < 2 * part_min || threads_.empty()) {  // not worth a hand-off
-        for (const Piece& p : pieces) std::memcpy(p.dst, p.src, p.len);
+        copy_pieces(pieces.data(), pieces.data() + pieces.size());
         return;
     }
     // Parts of about total / (2 x threads), at least part_min bytes.
@@ -206,7 +223,7 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
     for (const Piece& p : pieces)
         for (size_t o = 0; o < p.len; o += kPart) {
             const size_t len = std::min(kPart, p.len - o);
-            job.pieces.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o, len});
+            job.pieces.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o, len, p.nt});
             group += len;
             if (group >= group_bytes) {
                 job.bounds.push_back(job.pieces.size());

@@ -38,6 +38,7 @@ public:
         void* dst;
         const void* src;
         size_t len;
+        bool nt = false;  // dst is pinned staging a kernel reads next: stage_copy (+ fence)
     };
     // Copies every piece (split further into <= 1 MiB parts); returns when done.
     void run(const std::vector<Piece>& pieces);

@@ -310,6 +310,7 @@ struct rs_ctx {
     std::atomic<int64_t> encodes_in_place{0};                     // rs_encode from engine-pinned memory
     std::atomic<int64_t> decodes_in_place{0};                     // rs_decode from engine-pinned memory
     std::atomic<int64_t> rec_stripes_table{0}, rec_stripes_syndrome{0};  // launch_reconstruct's kernels (rs_stat)
+    std::atomic<int64_t> encode_batches{0};                              // rs_encode_batch calls through the GPU
     hipEvent_t pat_ev = nullptr;
     hipStream_t build_stream = nullptr;  // pattern builds (flush_patterns), off every caller's stream
     hipEvent_t caller_ev = nullptr;      // the building caller's stream tail (build_after_caller)
@@ -1726,6 +1727,7 @@ int64_t rs_stat(const rs_ctx* c, int which) {
         case RS_STAT_DECODES_IN_PLACE: return c->decodes_in_place.load();
         case RS_STAT_REC_STRIPES_TABLE: return c->rec_stripes_table.load();
         case RS_STAT_REC_STRIPES_SYNDROME: return c->rec_stripes_syndrome.load();
+        case RS_STAT_ENCODE_BATCHES: return c->encode_batches.load();
         case RS_STAT_LEASES: {
             std::lock_guard<std::mutex> lk(const_cast<rs_ctx*>(c)->lease_mu);
             return static_cast<int64_t>(c->leases.size());
@@ -2116,6 +2118,103 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     const int fin = finish(rc_dev);
     L.st_batch.release_after(s);
     return fin != RS_OK ? fin : rc;
+}
+
+// Pinned staging one rs_encode_batch group may use (inputs + parity); larger
+// batches go in groups, and a message that alone exceeds it takes rs_encode.
+constexpr size_t kEncBatchStage = size_t(512) << 20;
+
+int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t len, uint8_t* const* parities,
+                    int* status) {
+    if (!c || batch < 0 || (batch && (!inputs || !parities || !status))) return RS_EINVAL;
+    const size_t k = static_cast<size_t>(c->k), m = static_cast<size_t>(c->m);
+    if (len % k != 0) {
+        for (int b = 0; b < batch; ++b) status[b] = RS_ELEN_NOT_MULTIPLE;
+        return batch ? RS_ELEN_NOT_MULTIPLE : RS_OK;
+    }
+    const size_t S = len / k;
+    int rc = RS_OK;
+    std::vector<int> todo;
+    for (int b = 0; b < batch; ++b) {
+        status[b] = RS_OK;
+        if (S == 0 || m == 0) continue;
+        if (!inputs[b] || !parities[b]) {
+            status[b] = RS_EINVAL;
+            if (rc == RS_OK) rc = RS_EINVAL;
+            continue;
+        }
+        todo.push_back(b);
+    }
+    if (todo.empty()) return rc;
+    // Messages stripe by stripe in the strided layout, [group][k][pitch] in
+    // pinned staging followed by [group][m][pitch] of parity.
+    const size_t pitch = round_up(S, 64);
+    const size_t per_msg = (k + m) * pitch;
+    if (per_msg > kEncBatchStage || round_up(S, 16) / 16 >= (size_t(1) << 28)) {
+        for (int b : todo) {
+            status[b] = rs_encode(c, inputs[b], len, parities[b]);
+            if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
+        }
+        return rc;
+    }
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    Lease& L = *lg.L;
+    rsmi::HostPipeline* pipe = L.pipeline();
+    if (!pipe) return RS_ENOMEM;
+    const hipStream_t s = L.stream;
+    const size_t group = std::max<size_t>(1, kEncBatchStage / per_msg);
+    for (size_t g0 = 0; g0 < todo.size(); g0 += group) {
+        const size_t B = std::min(group, todo.size() - g0);
+        if (!L.st_batch.acquire(B * per_msg)) return RS_ENOMEM;
+        uint8_t* h_in = static_cast<uint8_t*>(L.st_batch.p);
+        uint8_t* h_out = h_in + B * k * pitch;
+        uint8_t* d_in = static_cast<uint8_t*>(L.st_batch.dev);
+        uint8_t* d_out = d_in + B * k * pitch;
+        L.begin(s);
+        // Chunks of messages: the staging copy of chunk i + 1 (copy pool,
+        // non-temporal) runs while the kernel codes chunk i over PCIe, and
+        // chunk i's parity is copied out while chunk i + 1's kernel runs.
+        const size_t nch = std::min<size_t>(B, B * k * pitch >= kBatchChunkMin ? kBatchChunks : 1);
+        hipError_t e = hipSuccess;
+        size_t launched = 0;
+        for (size_t ch = 0; ch < nch && e == hipSuccess; ++ch) {
+            const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+            std::vector<rsmi::CopyPool::Piece> in;
+            in.reserve((j1 - j0) * k);
+            for (size_t j = j0; j < j1; ++j)
+                for (size_t i = 0; i < k; ++i)
+                    in.push_back({h_in + (j * k + i) * pitch, inputs[todo[g0 + j]] + i * S, S, true});
+            pipe->copy(in);
+            rsmi::MatArgs a = base_args(c, d_in + j0 * k * pitch, k * pitch, d_out + j0 * m * pitch, m * pitch, pitch, S,
+                                        j1 - j0);
+            set_patterns(c, 1, c->d_encpat.p, a);
+            a.stripe_desc = nullptr;
+            e = launch_encode(c, a, s);
+            if (e == hipSuccess) e = hipEventRecord(L.ev[ch], s);
+            if (e == hipSuccess) ++launched;
+        }
+        L.end(s);
+        for (size_t ch = 0; ch < launched && e == hipSuccess; ++ch) {
+            e = rsmi::wait_event(L.ev[ch]);
+            if (e != hipSuccess) break;
+            const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+            std::vector<rsmi::CopyPool::Piece> out;
+            out.reserve((j1 - j0) * m);
+            for (size_t j = j0; j < j1; ++j)
+                for (size_t t = 0; t < m; ++t) out.push_back({parities[todo[g0 + j]] + t * S, h_out + (j * m + t) * pitch, S});
+            pipe->copy(out);
+        }
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(s);  // nothing may still read the staging
+            for (size_t j = g0; j < todo.size(); ++j) status[todo[j]] = RS_EDEVICE;
+            return RS_EDEVICE;
+        }
+    }
+    c->encode_batches += 1;
+    return rc;
 }
 
 int rs_blake2b_device(rs_ctx* c, int count, const uint64_t* msg_ptrs, const uint64_t* lens, const uint32_t* order,

@@ -260,6 +260,65 @@ func (f *FEC) DecodeBatch(msgs [][]Share) ([][]byte, []error) {
 	return outs, errs
 }
 
+// EncodeBatch is send-side batching (not in infectious): the parity of many
+// equal-length messages in one GPU pass (rs_encode_batch).  parities[b] holds
+// the n-k parity shares of inputs[b] back to back (share k+t at
+// [t*S, (t+1)*S)); the data shares are inputs[b]'s own slices, as Encode
+// emits them.
+func (f *FEC) EncodeBatch(inputs [][]byte) (parities [][]byte, errs []error) {
+	B := len(inputs)
+	parities = make([][]byte, B)
+	errs = make([]error, B)
+	if B == 0 {
+		return parities, errs
+	}
+	size := len(inputs[0])
+	for b, in := range inputs {
+		if len(in) != size {
+			errs[b] = errors.New("infectious: messages have different lengths")
+		}
+	}
+	for _, e := range errs {
+		if e != nil {
+			return parities, errs
+		}
+	}
+	m := f.n - f.k
+	plen := 0
+	if size%f.k == 0 {
+		plen = size / f.k * m
+	}
+	ins := (*[1 << 28]*C.uint8_t)(C.malloc(C.size_t(B) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:B:B]
+	outs := (*[1 << 28]*C.uint8_t)(C.malloc(C.size_t(B) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:B:B]
+	codes := (*[1 << 28]C.int)(C.malloc(C.size_t(B) * C.size_t(unsafe.Sizeof(C.int(0)))))[:B:B]
+	defer C.free(unsafe.Pointer(&ins[0]))
+	defer C.free(unsafe.Pointer(&outs[0]))
+	defer C.free(unsafe.Pointer(&codes[0]))
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	for b, in := range inputs {
+		parities[b] = make([]byte, plen)
+		ins[b], outs[b] = nil, nil
+		if size > 0 {
+			pinner.Pin(&in[0])
+			ins[b] = (*C.uint8_t)(unsafe.Pointer(&in[0]))
+		}
+		if plen > 0 {
+			pinner.Pin(&parities[b][0])
+			outs[b] = (*C.uint8_t)(unsafe.Pointer(&parities[b][0]))
+		}
+	}
+	C.rs_encode_batch(f.ctx, C.int(B), (**C.uint8_t)(unsafe.Pointer(&ins[0])), C.size_t(size),
+		(**C.uint8_t)(unsafe.Pointer(&outs[0])), &codes[0])
+	for b := range inputs {
+		if codes[b] != C.RS_OK {
+			errs[b] = statusErr(codes[b])
+			parities[b] = nil
+		}
+	}
+	return parities, errs
+}
+
 // Arena is engine-pinned receive memory (rs_arena).  Shards unmarshalled
 // into it are read in place by the GPU.  Not safe for concurrent use: one
 // arena per receiving goroutine; Reset once its messages are decoded.

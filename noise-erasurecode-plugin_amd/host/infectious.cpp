@@ -59,6 +59,28 @@ Status FEC::Encode(const uint8_t* input, size_t len,
     return Status::Ok();
 }
 
+Status FEC::EncodeBatch(const std::vector<const uint8_t*>& inputs, size_t len,
+                        std::vector<std::vector<uint8_t>>* parity, std::vector<Status>* st) {
+    const int B = static_cast<int>(inputs.size());
+    parity->assign(B, {});
+    st->assign(B, Status::Ok());
+    if (B == 0) return Status::Ok();
+    const size_t P = len % static_cast<size_t>(k_) == 0 ? len / static_cast<size_t>(k_) * (n_ - k_) : 0;
+    std::vector<uint8_t*> outs(B);
+    for (int b = 0; b < B; ++b) {
+        (*parity)[b].resize(P);
+        outs[b] = (*parity)[b].data();
+    }
+    std::vector<int> codes(B, RS_OK);
+    const int rc = rs_encode_batch(ctx_, B, inputs.data(), len, outs.data(), codes.data());
+    for (int b = 0; b < B; ++b)
+        if (codes[b] != RS_OK) {
+            (*st)[b] = from(codes[b], "Encode");
+            (*parity)[b].clear();
+        }
+    return rc == RS_OK ? Status::Ok() : from(rc, "EncodeBatch");
+}
+
 Status FEC::Decode(std::vector<uint8_t>* dst, std::vector<Share>& shares) {
     const int cnt = static_cast<int>(shares.size());
     const size_t S = cnt ? shares[0].Data.size() : 0;

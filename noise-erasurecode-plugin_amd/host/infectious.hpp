@@ -57,6 +57,11 @@ public:
     // Calls output for shares 0..n-1 in order (data shares first).
     Status Encode(const uint8_t* input, size_t len,
                   const std::function<void(const ShareView&)>& output);
+    // The parity of many messages of len bytes each in one GPU pass
+    // (rs_encode_batch): (*parity)[b] = the m * len / k parity bytes of
+    // inputs[b] (rs_encode's layout), (*st)[b] its status.
+    Status EncodeBatch(const std::vector<const uint8_t*>& inputs, size_t len,
+                       std::vector<std::vector<uint8_t>>* parity, std::vector<Status>* st);
     // Sorts `shares` by Number in place; *dst receives k * len(share) bytes.
     Status Decode(std::vector<uint8_t>* dst, std::vector<Share>& shares);
     // Decode of many messages (same share length) in one GPU pass

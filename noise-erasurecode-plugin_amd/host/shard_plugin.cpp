@@ -209,21 +209,41 @@ void ShardPlugin::prepareShardsBatch(const PeerID& self, const std::vector<std::
         }
         for (size_t i = 0; i < inputs.size(); ++i) sigs[i] = sign_(h[i]);
     }
-    for (size_t i = 0; i < inputs.size(); ++i) {
-        std::vector<Share> shares;
-        Status st = shardInput(inputs[i], &shares);
-        if (!st.ok()) {
-            (*sts)[i] = st;
-            continue;
-        }
-        for (Share& s : shares) {
-            Shard m;
-            m.FileSignature = sigs[i];
-            m.ShardData = std::move(s.Data);
-            m.ShardNumber = static_cast<uint64_t>(s.Number);
-            m.TotalShards = static_cast<uint64_t>(TotalShards);
-            m.MinimumNeededShards = static_cast<uint64_t>(MinimumNeededShards);
-            (*out)[i].push_back(std::move(m));
+    // The encodes: messages of equal length go through one rs_encode_batch
+    // pass each (send-side batching); then shardInput's shares per message
+    // (data shares copied out of the input, main.go:255-258).
+    std::shared_ptr<FEC> f;
+    Status fs = CachedFEC(MinimumNeededShards, TotalShards, &f);
+    if (!fs.ok()) {
+        sts->assign(inputs.size(), fs);
+        return;
+    }
+    std::map<size_t, std::vector<size_t>> by_len;
+    for (size_t i = 0; i < inputs.size(); ++i) by_len[inputs[i].size()].push_back(i);
+    const size_t k = static_cast<size_t>(MinimumNeededShards), m = static_cast<size_t>(TotalShards) - k;
+    for (const auto& [len, idx] : by_len) {
+        std::vector<const uint8_t*> ptrs;
+        for (size_t i : idx) ptrs.push_back(inputs[i].data());
+        std::vector<std::vector<uint8_t>> parity;
+        std::vector<Status> est;
+        f->EncodeBatch(ptrs, len, &parity, &est);
+        for (size_t q = 0; q < idx.size(); ++q) {
+            const size_t i = idx[q];
+            if (!est[q].ok()) {
+                (*sts)[i] = est[q];
+                continue;
+            }
+            const size_t S = len / k;
+            for (size_t sn = 0; sn < k + m; ++sn) {
+                Shard sh;
+                sh.FileSignature = sigs[i];
+                const uint8_t* src = sn < k ? inputs[i].data() + sn * S : parity[q].data() + (sn - k) * S;
+                sh.ShardData.assign(src, src + S);
+                sh.ShardNumber = static_cast<uint64_t>(sn);
+                sh.TotalShards = static_cast<uint64_t>(TotalShards);
+                sh.MinimumNeededShards = static_cast<uint64_t>(MinimumNeededShards);
+                (*out)[i].push_back(std::move(sh));
+            }
         }
     }
 }

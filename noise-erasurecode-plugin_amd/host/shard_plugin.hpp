@@ -127,8 +127,9 @@ public:
     Status prepareShards(const PeerID& self, const std::vector<uint8_t>* input,
                          std::vector<Shard>* out);
     // prepareShards for many inputs: every input's signature hash in one
-    // rs_blake2b call (HashLen > 0), then shardInput per input.  (*out)[i] / (*sts)[i]
-    // correspond to inputs[i].
+    // rs_blake2b call (HashLen > 0), and the encodes of equal-length inputs
+    // in one rs_encode_batch pass each (send-side batching); shares as
+    // shardInput makes them.  (*out)[i] / (*sts)[i] correspond to inputs[i].
     void prepareShardsBatch(const PeerID& self, const std::vector<std::vector<uint8_t>>& inputs,
                             std::vector<std::vector<Shard>>* out, std::vector<Status>* sts);
     // main.go:243-267

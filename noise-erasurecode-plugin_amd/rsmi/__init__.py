@@ -35,7 +35,7 @@ RS_ETOO_MANY_ERRORS = -16
 # Every symbol include/rsmi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (
     "rs_new", "rs_new_on_device", "rs_free", "rs_k", "rs_n", "rs_device",
-    "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode", "rs_decode_batch",
+    "rs_encode_matrix", "rs_strerror", "rs_encode", "rs_decode", "rs_decode_batch", "rs_encode_batch",
     "rs_encode_stripes", "rs_reconstruct_stripes", "rs_reconstruct_ptrs", "rs_pattern_count",
     "rs_pattern_evictions",
     "rs_prepare_patterns",
@@ -87,6 +87,7 @@ def _lib() -> ctypes.CDLL:
             "rs_decode": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(vp), i32, sz, vp]),
             "rs_decode_batch": (i32, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32),
                                       ctypes.POINTER(vp), sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
+            "rs_encode_batch": (i32, [vp, i32, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
             "rs_encode_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp]),
             "rs_reconstruct_stripes": (i32, [vp, vp, sz, vp, sz, sz, sz, sz, vp, vp]),
             "rs_reconstruct_ptrs": (i32, [vp, vp, sz, sz, vp, vp]),
@@ -269,6 +270,29 @@ class FEC:
         return ([bytes(o[:self.k * S]) if st[b] == RS_OK else None for b, o in enumerate(outs)],
                 [st[b] for b in range(B)])
 
+    def EncodeBatch(self, inputs: List[bytes]):
+        """rs_encode_batch: the parity of many equal-length messages in one
+        GPU pass (send-side batching).  Returns (parities, statuses);
+        parities[b] is the m*S parity bytes (rs_encode's layout) or None where
+        statuses[b] != 0."""
+        B = len(inputs)
+        L = len(inputs[0]) if B else 0
+        for x in inputs:
+            if len(x) != L:
+                raise RSError(RS_EINVAL, "EncodeBatch: messages of unequal length")
+        m = self.n - self.k
+        P = (L // self.k) * m if L % self.k == 0 else 0
+        keep = [bytes(x) for x in inputs]
+        ins = (ctypes.c_void_p * max(B, 1))(
+            *[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value for b in keep])
+        outs = [bytearray(max(P, 1)) for _ in range(B)]
+        outp = (ctypes.c_void_p * max(B, 1))(
+            *[ctypes.addressof((ctypes.c_char * len(o)).from_buffer(o)) for o in outs])
+        st = (ctypes.c_int * max(B, 1))()
+        _lib().rs_encode_batch(self._h, B, ins, L, outp, st)
+        return ([bytes(o[:P]) if st[b] == RS_OK else None for b, o in enumerate(outs)],
+                [st[b] for b in range(B)])
+
     # -- device-resident batched API -------------------------------------------
     def encode_stripes(self, data_ptr: int, data_stride: int, parity_ptr: int,
                        parity_stride: int, pitch: int, shard_len: int, stripes: int,
@@ -305,7 +329,8 @@ class FEC:
         return _lib().rs_pattern_count(self._h)
 
     (STAT_PATTERNS, STAT_EVICTIONS, STAT_BATCHES_IN_PLACE, STAT_BATCHES_STAGED, STAT_LEASES,
-     STAT_ENCODES_IN_PLACE, STAT_DECODES_IN_PLACE, STAT_REC_STRIPES_TABLE, STAT_REC_STRIPES_SYNDROME) = range(9)
+     STAT_ENCODES_IN_PLACE, STAT_DECODES_IN_PLACE, STAT_REC_STRIPES_TABLE, STAT_REC_STRIPES_SYNDROME,
+     STAT_ENCODE_BATCHES) = range(10)
 
     def stat(self, which: int) -> int:
         return _lib().rs_stat(self._h, which)

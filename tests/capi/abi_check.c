@@ -8,7 +8,7 @@
  * Encode main.go:262 -> rs_encode (config 1 blob); Decode main.go:77 ->
  * rs_decode with shares in arrival order (sorted in place); receive-side
  * batching -> rs_decode_batch with ShardData unmarshalled into an rs_arena
- * (zero-copy); the blake2b hash policy -> rs_blake2b_batch (RFC 7693 known
+ * (zero-copy); send-side batching -> rs_encode_batch; the blake2b hash policy -> rs_blake2b_batch (RFC 7693 known
  * answers); error classes; 8 pthreads decoding on one context.
  */
 #include <pthread.h>
@@ -65,6 +65,33 @@ static void check_encode_decode(rs_ctx *ctx, int k, int n, size_t len, uint64_t 
     CHECK(memcmp(out, in, len) == 0, "decoded != input (k=%d n=%d)", k, n);
     for (int i = 1; i < k; i++) CHECK(nums[i - 1] < nums[i], "numbers not sorted in place");
     free(in); free(par); free(ref); free(out);
+}
+
+/* Send-side batching: B messages' parity in one rs_encode_batch call, each
+ * against the oracle (the way a cgo sender would call it). */
+static void check_encode_batch(rs_ctx *ctx, int k, int n, size_t len, int B) {
+    const int m = n - k;
+    const size_t S = len / k;
+    uint8_t enc[256 * 256];
+    orc_fec_matrix(k, n, 1, enc);
+    const uint8_t *ins[64];
+    uint8_t *outs[64];
+    int st[64];
+    for (int b = 0; b < B; b++) {
+        ins[b] = splitmix(len, 0xBA7 + (uint64_t)b);
+        outs[b] = malloc(m * S);
+    }
+    const int64_t batches0 = rs_stat(ctx, RS_STAT_ENCODE_BATCHES);
+    CHECK(rs_encode_batch(ctx, B, ins, len, outs, st) == RS_OK, "rs_encode_batch");
+    CHECK(rs_stat(ctx, RS_STAT_ENCODE_BATCHES) == batches0 + 1, "rs_encode_batch not batched");
+    uint8_t *ref = malloc(m * S);
+    for (int b = 0; b < B; b++) {
+        CHECK(orc_encode(enc, k, n, ins[b], len, ref) == 0, "orc_encode");
+        CHECK(st[b] == RS_OK && memcmp(outs[b], ref, m * S) == 0, "encode batch message %d (k=%d n=%d)", b, k, n);
+        free((void *)ins[b]);
+        free(outs[b]);
+    }
+    free(ref);
 }
 
 /* Receive batching: marshalled Shards unmarshalled into an arena, decoded in
@@ -190,6 +217,8 @@ int main(void) {
     check_encode_decode(c10, 10, 14, 10 * 17, 3);
     check_encode_decode(c64, 64, 80, 64 * 4099, 4);
     check_encode_decode(c4, 4, 6, 64, 5);              /* plugin default RS(4,2) */
+    check_encode_batch(c10, 10, 14, 1048580, 24);     /* config-1 messages, chunked staging */
+    check_encode_batch(c64, 64, 80, 64 * 4099, 5);
     check_arena_batch(c10, 10, 14, 6554, 64);
     check_arena_batch(c64, 64, 80, 4099, 8);
     check_blake2b(c10);

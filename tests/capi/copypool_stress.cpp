@@ -7,8 +7,11 @@
 // a few multi-MiB ones that the pool splits into parts -- at the same time,
 // the way concurrent rs_encode/rs_decode/rs_decode_batch calls on one context
 // (or on several contexts in one process) share the pool.  Every destination
-// must equal its source byte for byte; the sanitizers flag any data race on
-// the job queue or out-of-bounds part split.
+// must equal its source byte for byte (starts misaligned on both sides, half
+// the pieces through the non-temporal staging copy, guard bytes untouched);
+// the sanitizers flag any data race on the job queue or out-of-bounds part
+// split or copy.
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -30,17 +33,28 @@ int main(int argc, char** argv) {
             for (int it = 0; it < iters; ++it) {
                 const int np = 1 + static_cast<int>(rng() % 64);
                 std::vector<std::vector<unsigned char>> src(np), dst(np);
+                std::vector<size_t> lens(np), soff(np), doff(np);
                 std::vector<rsmi::CopyPool::Piece> pieces;
                 for (int i = 0; i < np; ++i) {
                     const size_t len = rng() % 3 == 0 ? rng() % (3u << 20) : rng() % 70000;
-                    src[i].resize(len);
-                    for (size_t j = 0; j < len; j += 997) src[i][j] = static_cast<unsigned char>(rng());
-                    dst[i].assign(len, 0xA5);
-                    pieces.push_back({dst[i].data(), src[i].data(), len});
+                    // misaligned starts on both sides (the non-temporal copy's
+                    // head / body / tail split), 32 guard bytes past the end
+                    lens[i] = len;
+                    soff[i] = rng() % 16;
+                    doff[i] = rng() % 16;
+                    src[i].resize(len + soff[i]);
+                    for (size_t j = 0; j < src[i].size(); j += 997) src[i][j] = static_cast<unsigned char>(rng());
+                    dst[i].assign(len + doff[i] + 32, 0xA5);
+                    const bool nt = rng() % 2 == 0;  // staging-bound pieces (stage_copy + fence)
+                    pieces.push_back({dst[i].data() + doff[i], src[i].data() + soff[i], len, nt});
                 }
                 pool.run(pieces);
-                for (int i = 0; i < np; ++i)
-                    if (src[i] != dst[i]) bad.fetch_add(1);
+                for (int i = 0; i < np; ++i) {
+                    bool ok = std::equal(src[i].begin() + soff[i], src[i].end(), dst[i].begin() + doff[i]);
+                    for (size_t j = 0; j < doff[i]; ++j) ok &= dst[i][j] == 0xA5;
+                    for (size_t j = doff[i] + lens[i]; j < dst[i].size(); ++j) ok &= dst[i][j] == 0xA5;
+                    if (!ok) bad.fetch_add(1);
+                }
             }
         });
     for (auto& x : th) x.join();

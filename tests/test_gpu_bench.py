@@ -65,6 +65,7 @@ def test_bench_single_gpu_extra_legs(torch_dev):
     assert c1["message_bytes"] == 1048580 and len(c1["dropped"]) == 4
     assert c1["codec"]["encode_ms"] > 0 and c1["codec"]["decode4_ms"] > 0 and c1["codec"]["decode4_arena_ms"] > 0
     assert c1["codec"]["decode4_batch64_ms_per_message"] > 0
+    assert c1["codec"]["encode_batch64_ms_per_message"] > 0 and c1["gpu_vs_1core"]["encode_batch64"] > 0
     assert set(c1["cpu_1t"]) == {"scalar_1t", "avx2_1t"}
     c5 = d["config5"]
     assert c5["status"] == "ok", c5

@@ -1,0 +1,127 @@
+"""GPU: rs_encode_batch (send-side batching) against the oracle.
+
+Many messages' Encode (main.go:262, called once per message by shardInput,
+main.go:243-267) in one GPU pass: every message's parity must equal the
+oracle's encode of it, and equal what rs_encode gives one message at a time.
+Covers the split-table codes and the bit-sliced ones, ragged shard lengths
+(the staging pitch pads them), batches staged in one chunk and in several,
+and the error statuses (length not a multiple of k, a null message).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import rsmi  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+_FECS = {}
+
+
+def fec(k, n):
+    if (k, n) not in _FECS:
+        _FECS[(k, n)] = rsmi.NewFEC(k, n)
+    return _FECS[(k, n)]
+
+
+def _messages(k, S, B, seed):
+    return [oracle.splitmix_bytes(k * S, seed + 977 * b).tobytes() for b in range(B)]
+
+
+@pytest.mark.parametrize("k,n,S,B", [
+    (10, 14, 1, 5), (10, 14, 17, 9), (10, 14, 4099, 33), (10, 14, 104858, 7),
+    (4, 6, 4096, 64), (8, 14, 6553, 11), (64, 80, 4099, 6), (17, 49, 1000, 5), (1, 2, 333, 4),
+])
+def test_encode_batch_matches_oracle(k, n, S, B):
+    f = fec(k, n)
+    E = oracle.fec_matrix(k, n)
+    msgs = _messages(k, S, B, 100 * k + S)
+    before = f.stat(rsmi.FEC.STAT_ENCODE_BATCHES)
+    par, st = f.EncodeBatch(msgs)
+    assert st == [0] * B
+    for b in range(B):
+        assert par[b] == oracle.encode(E, k, n, msgs[b]), b
+    assert f.stat(rsmi.FEC.STAT_ENCODE_BATCHES) == before + 1
+
+
+def test_encode_batch_chunked_config1_messages():
+    """20 config-1 messages (>= 16 MiB staged: four chunks, each coded while
+    the next is copied in), against rs_encode one message at a time."""
+    k, n = 10, 14
+    f = fec(k, n)
+    S = 104858
+    msgs = _messages(k, S, 20, 7)
+    par, st = f.EncodeBatch(msgs)
+    assert st == [0] * 20
+    E = oracle.fec_matrix(k, n)
+    for b in (0, 5, 19):
+        assert par[b] == oracle.encode(E, k, n, msgs[b])
+    for b in range(20):
+        assert par[b] == f.encode_parity(msgs[b])
+
+
+def test_encode_batch_large_shards_past_a_group():
+    """Messages whose staging exceeds one group's budget go through several
+    groups (RS(10,4), 4 MiB shards: 56 MiB per message)."""
+    k, n = 10, 14
+    f = fec(k, n)
+    S = 4 << 20
+    msgs = _messages(k, S, 10, 3)
+    par, st = f.EncodeBatch(msgs)
+    assert st == [0] * 10
+    E = oracle.fec_matrix(k, n)
+    for b in (0, 9):  # the first group and the last
+        assert par[b] == oracle.encode(E, k, n, msgs[b])
+    for b in range(10):
+        assert par[b] == f.encode_parity(msgs[b])
+
+
+def test_encode_batch_errors_and_edges():
+    k, n = 10, 14
+    f = fec(k, n)
+    lib = rsmi.load()
+    # len not a multiple of k: every message fails the same way
+    par, st = f.EncodeBatch([b"x" * 13, b"y" * 13])
+    assert st == [rsmi.RS_ELEN_NOT_MULTIPLE] * 2 and par == [None, None]
+    # empty messages: nothing to code
+    par, st = f.EncodeBatch([b"", b""])
+    assert st == [0, 0] and par == [b"", b""]
+    # an empty batch
+    assert f.EncodeBatch([]) == ([], [])
+    # a null message among good ones: only it fails
+    S = 4096
+    msgs = _messages(k, S, 3, 11)
+    keep = [bytes(m) for m in msgs]
+    ins = (ctypes.c_void_p * 3)(ctypes.cast(ctypes.c_char_p(keep[0]), ctypes.c_void_p).value, None,
+                                ctypes.cast(ctypes.c_char_p(keep[2]), ctypes.c_void_p).value)
+    outs = [bytearray(4 * S) for _ in range(3)]
+    outp = (ctypes.c_void_p * 3)(*[ctypes.addressof((ctypes.c_char * len(o)).from_buffer(o)) for o in outs])
+    st = (ctypes.c_int * 3)()
+    rc = lib.rs_encode_batch(f.handle, 3, ins, k * S, outp, st)
+    assert rc == rsmi.RS_EINVAL and list(st) == [0, rsmi.RS_EINVAL, 0]
+    E = oracle.fec_matrix(k, n)
+    assert bytes(outs[0]) == oracle.encode(E, k, n, keep[0])
+    assert bytes(outs[2]) == oracle.encode(E, k, n, keep[2])
+    # bad arguments
+    assert lib.rs_encode_batch(None, 1, ins, k * S, outp, st) == rsmi.RS_EINVAL
+    assert lib.rs_encode_batch(f.handle, -1, ins, k * S, outp, st) == rsmi.RS_EINVAL
+
+
+def test_encode_batch_messages_alias_nothing_between_calls():
+    """Back-to-back batches on one context (the lease's staging reused) give
+    each batch its own parity."""
+    k, n = 10, 14
+    f = fec(k, n)
+    E = oracle.fec_matrix(k, n)
+    for rep in range(4):
+        msgs = _messages(k, 6554 + 16 * rep, 24, 1000 + rep)
+        par, st = f.EncodeBatch(msgs)
+        assert st == [0] * 24
+        assert par[rep] == oracle.encode(E, k, n, msgs[rep])
+        assert par[-1] == oracle.encode(E, k, n, msgs[-1])

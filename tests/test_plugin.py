@@ -432,6 +432,28 @@ def test_prepare_shards_batch_matches_single():
     assert p.HashBytes([b"abc"]) == [hashlib.blake2b(b"abc", digest_size=32).digest()]
 
 
+def test_prepare_shards_batch_equal_lengths_one_pass():
+    """Equal-length inputs are encoded in one rs_encode_batch pass per length
+    (send-side batching): every message's Shards equal prepareShards' and
+    their parity the oracle's; a length that is not a multiple of k fails
+    alone."""
+    k, n = 10, 14
+    p = h.NewShardPlugin(None, None, k, n)
+    E = oracle.fec_matrix(k, n)
+    inputs = [oracle.splitmix_bytes(1048580, 500 + i).tobytes() for i in range(12)]
+    inputs += [oracle.splitmix_bytes(10 * 4099, 700 + i).tobytes() for i in range(5)] + [b"0123456789a"]
+    out, codes = p.prepareShardsBatch(SELF, inputs)
+    assert codes[-1] != 0 and all(c == 0 for c in codes[:-1])
+    for i, (inp, shards) in enumerate(zip(inputs[:-1], out[:-1])):
+        assert shards == p.prepareShards(SELF, inp), i
+        S = len(inp) // k
+        assert [s.ShardNumber for s in shards] == list(range(n))
+        assert b"".join(s.ShardData for s in shards[:k]) == inp
+        if i in (0, 11, 12, 16):
+            assert b"".join(s.ShardData for s in shards[k:]) == oracle.encode(E, k, n, inp)
+        assert all(len(s.ShardData) == S for s in shards)
+
+
 def test_prepare_shards_hash_overlaps_encode():
     """prepareShards of the config-1 blob with the hash
     policy costs about one host hash (the GPU encode runs beside it), not a
