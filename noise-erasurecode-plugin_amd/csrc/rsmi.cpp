@@ -2035,6 +2035,88 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     rsmi::HostPipeline* pipe = L.pipeline();
     if (!pipe) return RS_ENOMEM;
     const hipStream_t s = L.stream;
+    static const bool batch_dma = [] {
+        const char* e = std::getenv("RSMI_BATCH_DMA");  // 1: stage survivors by DMA (round 4; A/B)
+        return e && std::atoi(e) != 0;
+    }();
+    if (!batch_dma) {
+        // Survivors read by the kernel over PCIe where they are (engine-pinned,
+        // in_place) or where the copy pool staged them (non-temporal stores),
+        // in chunks of messages: chunk i is reconstructed while chunk i + 1
+        // is staged and chunk i - 1's regenerated data shards -- written by
+        // the kernel into pinned staging -- are copied out; erased parity (not
+        // returned) goes to a device scratch row.  No DMA: the round-4 form
+        // queued every chunk's H2D, then the kernel, then the D2H
+        // (RSMI_BATCH_DMA=1).
+        const size_t sp = round_up(S, 64);
+        const size_t in_bytes = in_place ? 0 : B * static_cast<size_t>(k) * sp;
+        const size_t tbl = B * static_cast<size_t>(n) * sizeof(uint64_t);
+        if (!L.st_batch.acquire(in_bytes + std::max<size_t>(E, 1) * sp) || !L.st_pieces.acquire(tbl) ||
+            !L.d_pieces.reserve_on(tbl, s) || !L.d_batch.reserve_on(std::max<size_t>(n_par_out, 1) * sp, s))
+            return RS_ENOMEM;
+        uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
+        uint8_t* hd = static_cast<uint8_t*>(L.st_batch.dev);
+        uint8_t* h_out = h + in_bytes;
+        uint8_t* d_out = hd + in_bytes;
+        uint8_t* d_par = static_cast<uint8_t*>(L.d_batch.p);
+        uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
+        std::vector<rsmi::CopyPool::Piece> stage_in;
+        stage_in.reserve(B * static_cast<size_t>(k));
+        size_t r_data = 0, r_par = 0;
+        for (size_t j = 0; j < B; ++j) {
+            size_t q = 0;
+            for (int i = 0; i < n; ++i) {
+                uint64_t& t = tab[j * n + i];
+                if (const uint8_t* p = by[fast[j]][i]) {
+                    const size_t slot = j * k + q++;
+                    if (in_place) {
+                        t = dev_of[j * n + i];
+                    } else {
+                        stage_in.push_back({h + slot * sp, p, S, true});
+                        t = reinterpret_cast<uint64_t>(hd + slot * sp);
+                    }
+                } else if (i < k) {
+                    t = reinterpret_cast<uint64_t>(d_out + r_data++ * sp);
+                } else {
+                    t = reinterpret_cast<uint64_t>(d_par + r_par++ * sp);
+                }
+            }
+        }
+        auto finish = [&](int code) {
+            if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
+            return code;
+        };
+        L.begin(s);
+        if (hipMemcpyAsync(L.d_pieces.p, tab, tbl, hipMemcpyHostToDevice, s) != hipSuccess) return finish(RS_EDEVICE);
+        L.st_pieces.release_after(s);
+        const size_t moved = B * static_cast<size_t>(k) * sp;  // survivor bytes the kernels read
+        const size_t nch = std::min<size_t>(B, moved >= kBatchChunkMin ? kBatchChunks : 1);
+        std::vector<size_t> rows_before(B + 1, 0);  // regenerated data rows of messages [0, j)
+        for (size_t j = 0; j < B; ++j) {
+            size_t e_j = 0;
+            for (int i = 0; i < k; ++i) e_j += by[fast[j]][i] == nullptr;
+            rows_before[j + 1] = rows_before[j] + e_j;
+        }
+        size_t launched = 0;
+        for (size_t ch = 0; ch < nch; ++ch) {
+            const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+            if (!in_place)
+                pipe->copy(std::vector<rsmi::CopyPool::Piece>(stage_in.begin() + j0 * k, stage_in.begin() + j1 * k));
+            const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, sp, S, j1 - j0, erased.data() + j0 * n,
+                                       static_cast<const uint64_t*>(L.d_pieces.p) + j0 * n, s);
+            if (st != RS_OK || hipEventRecord(L.ev[ch], s) != hipSuccess) return finish(st != RS_OK ? st : RS_EDEVICE);
+            ++launched;
+        }
+        pipe->copy(direct);  // present data shards: no GPU, while it works
+        for (size_t ch = 0; ch < launched; ++ch) {
+            if (rsmi::wait_event(L.ev[ch]) != hipSuccess) return finish(RS_EDEVICE);
+            const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+            std::vector<rsmi::CopyPool::Piece> out;
+            for (size_t r = rows_before[j0]; r < rows_before[j1]; ++r) out.push_back({regen[r], h_out + r * sp, S});
+            pipe->copy(out);
+        }
+        return rc;
+    }
     L.begin(s);  // the lease's buffers may last have been read on another stream
     const size_t table_bytes = B * static_cast<size_t>(n) * sizeof(uint64_t);
     if (!L.st_batch.acquire(std::max<size_t>(std::max(packed, E * pitch), 16)) ||

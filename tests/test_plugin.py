@@ -534,3 +534,33 @@ def test_concurrent_receive_config1_blobs():
         dec = [e for e in mine if e[2]]
         assert len(dec) == 1 and dec[0][3] and dec[0][4] == blobs[b], b
         assert recv.PoolSize(sigs[b]) == 0  # verified: the pool was deleted (main.go:90-92)
+
+
+def test_decode_batch_dma_knob_matches():
+    """RSMI_BATCH_DMA=1 keeps round 4's DMA staging for rs_decode_batch (an
+    A/B knob): the same batch decodes to the same bytes through it (a child
+    process: the knob is read once per process)."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = ['.', 'noise-erasurecode-plugin_amd']\n"
+        "import numpy as np, rsmi\n"
+        "from oracle import oracle\n"
+        "k, n, S = 10, 14, 70001\n"
+        "f = rsmi.NewFEC(k, n); E = oracle.fec_matrix(k, n)\n"
+        "rng = np.random.default_rng(5); msgs, want = [], []\n"
+        "for b in range(40):\n"
+        "    d = oracle.splitmix_bytes(k * S, 70 + b).tobytes(); p = oracle.encode(E, k, n, d)\n"
+        "    sh = [d[i*S:(i+1)*S] for i in range(k)] + [p[i*S:(i+1)*S] for i in range(n - k)]\n"
+        "    keep = rng.choice(n, size=k, replace=False).tolist()\n"
+        "    msgs.append([rsmi.Share(i, sh[i]) for i in keep]); want.append(d)\n"
+        "outs, st = f.DecodeBatch(msgs)\n"
+        "assert outs == want and not any(st), st\n"
+        "assert f.stat(f.STAT_BATCHES_STAGED) == 1\n"
+        "print('ok')\n")
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for dma in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=180,
+                           env=dict(os.environ, RSMI_BATCH_DMA=dma))
+        assert r.returncode == 0 and "ok" in r.stdout, (dma, r.stdout, r.stderr[-2000:])
