@@ -5,8 +5,10 @@ oracle: random (k, n), shard lengths from 1 byte to past the one-shot staging
 threshold (aligned and ragged), k to n shares in random order, sometimes with
 one corrupted share (Correct / Berlekamp-Welch), survivors in pageable
 memory, in an engine-pinned rs_arena (read in place) or mixed, dst pageable
-or engine-pinned.  Every parity and every decoded message is compared with
-the oracle's.  Prints one JSON line.
+or engine-pinned.  Every fourth case also runs a batch of 1-40 messages of
+that shape through rs_encode_batch and rs_decode_batch (own shares, drops,
+corruptions and survivor placement per message).  Every parity and every
+decoded message is compared with the oracle's.  Prints one JSON line.
 
 usage: tools/fuzz_host_api.py [--seconds 120 | --cases N] [--seed 1]
 """
@@ -25,6 +27,60 @@ import numpy as np  # noqa: E402
 CODES = [(10, 14), (64, 80), (8, 14), (4, 6), (17, 49), (1, 3), (32, 40), (100, 120), (200, 256), (2, 4)]
 
 
+def batch_case(rng, lib, f, E, k, n, S, stats, oracle, rsmi):
+    """rs_encode_batch then rs_decode_batch over B messages of k*S bytes."""
+    m = n - k
+    P = ctypes.c_void_p
+    B = int(rng.integers(1, 41))
+    B = max(1, min(B, (24 << 20) // max(1, k * S)))
+    datas = [oracle.splitmix_bytes(k * S, int(rng.integers(0, 2**32))) for _ in range(B)]
+    pars = [np.zeros(m * S, dtype=np.uint8) for _ in range(B)]
+    ins = (ctypes.c_void_p * B)(*[d.ctypes.data for d in datas])
+    outs = (ctypes.c_void_p * B)(*[p_.ctypes.data for p_ in pars])
+    st = (ctypes.c_int * B)()
+    rc = lib.rs_encode_batch(f.handle, B, ins, k * S, outs, st)
+    assert rc == 0 and not any(st), f"k={k} n={n} S={S} B={B} encode_batch rc {rc} {list(st)[:4]}"
+    for b in range(B):
+        assert pars[b].tobytes() == oracle.encode(E, k, n, datas[b].tobytes()), f"k={k} n={n} S={S} B={B} batch parity {b}"
+    stats["encode_batch_msgs"] += B
+    # decode: per message its own share set (k or more), maybe one corrupted share
+    counts, nums, ptrs, keep, refs, arenas = [], [], [], [], [], []
+    in_arena = rng.random() < 0.4
+    arena = rsmi.Arena(B * n * (S + 256) + 4096) if in_arena else None
+    for b in range(B):
+        cnt = k if rng.random() < 0.7 else int(rng.integers(k, n + 1))
+        ids = [int(v) for v in rng.choice(n, size=cnt, replace=False)]
+        sh = {i: (datas[b][i * S:(i + 1) * S] if i < k else pars[b][(i - k) * S:(i - k + 1) * S]).copy() for i in ids}
+        if cnt >= k + 2 and rng.random() < 0.5:
+            v = ids[int(rng.integers(0, cnt))]
+            sh[v][int(rng.integers(0, S))] ^= np.uint8(1 + int(rng.integers(0, 255)))
+        shares = [(i, sh[i].tobytes()) for i in ids]
+        refs.append(oracle.decode(E, k, n, shares) if cnt == k else oracle.decode_correct(E, k, n, shares))
+        counts.append(cnt)
+        for i in ids:
+            nums.append(i)
+            if arena is not None:
+                ptrs.append(arena.put(sh[i].tobytes()))
+            else:
+                keep.append(sh[i])
+                ptrs.append(sh[i].ctypes.data)
+    dsts = [np.zeros(k * S, dtype=np.uint8) for _ in range(B)]
+    cc = (ctypes.c_int * B)(*counts)
+    nn = (ctypes.c_int * len(nums))(*nums)
+    pp = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    dd = (ctypes.c_void_p * B)(*[d.ctypes.data for d in dsts])
+    st = (ctypes.c_int * B)()
+    lib.rs_decode_batch(f.handle, B, cc, nn, pp, S, dd, st)
+    if arena is not None:
+        arena.free()
+    for b in range(B):
+        ref_rc, ref = refs[b]
+        assert (st[b] == 0) == (ref_rc == 0), f"k={k} n={n} S={S} B={B} decode_batch msg {b} rc {st[b]} vs {ref_rc}"
+        if st[b] == 0:
+            assert dsts[b].tobytes() == ref == datas[b].tobytes(), f"k={k} n={n} S={S} B={B} decode_batch msg {b} bytes"
+    stats["decode_batch_msgs"] += B
+
+
 def run(seconds=None, cases=None, seed=1):
     import rsmi
     from oracle import oracle
@@ -34,7 +90,7 @@ def run(seconds=None, cases=None, seed=1):
     P = ctypes.c_void_p
     fecs, mats = {}, {}
     stats = {"cases": 0, "encode": 0, "decode_k": 0, "decode_more": 0, "corrupted": 0, "arena": 0,
-             "pinned_dst": 0, "failures": 0}
+             "pinned_dst": 0, "encode_batch_msgs": 0, "decode_batch_msgs": 0, "failures": 0}
     first = []
     t0 = time.time()
     while (cases is None or stats["cases"] < cases) and (seconds is None or time.time() - t0 < seconds):
@@ -108,6 +164,8 @@ def run(seconds=None, cases=None, seed=1):
             if rc == 0:
                 assert got == ref, f"{case} cnt={cnt} corrupt={corrupt} decode bytes"
                 assert got == data.tobytes(), f"{case} cnt={cnt} corrupt={corrupt} not the message"
+            if stats["cases"] % 4 == 0:
+                batch_case(rng, lib, f, E, k, n, S, stats, oracle, rsmi)
         except AssertionError as e:
             stats["failures"] += 1
             if len(first) < 5:
