@@ -79,7 +79,7 @@ def test_concurrent_decode_one_fec(k, n, S):
 
 
 def test_concurrent_encode_and_decode_batch():
-    """Encode, Decode and DecodeBatch from different threads on one FEC."""
+    """Encode, DecodeBatch and EncodeBatch from different threads on one FEC."""
     k, n, S = 10, 14, 65536
     f = rsmi.FEC(k, n)
     E = oracle.fec_matrix(k, n)
@@ -104,8 +104,16 @@ def test_concurrent_encode_and_decode_batch():
             if s != 0 or o != data:
                 errors.append(("batch", j))
 
-    with ThreadPoolExecutor(6) as ex:
-        futs = [ex.submit(encoder, j) for j in range(6)] + [ex.submit(batcher, j) for j in range(4)]
+    def enc_batcher(j):
+        for _ in range(3):
+            pars, st = f.EncodeBatch([data for data, _ in msgs])
+            for (data, sh), p, s in zip(msgs, pars, st):
+                if s != 0 or p != b"".join(sh[k:]):
+                    errors.append(("encode_batch", j))
+
+    with ThreadPoolExecutor(8) as ex:
+        futs = ([ex.submit(encoder, j) for j in range(6)] + [ex.submit(batcher, j) for j in range(4)] +
+                [ex.submit(enc_batcher, j) for j in range(4)])
         for fu in futs:
             fu.result()
     assert not errors, errors[:5]
