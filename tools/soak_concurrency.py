@@ -3,8 +3,8 @@
 --shard 104858 gives config-1-sized messages, whose host-API calls take the
 two-chunk staged path) (SURVEY §8b threading): for
 --seconds, T threads mix every C-ABI entry point that shares the context's
-pattern cache -- rs_decode (host API), rs_decode_batch, rs_encode and
-rs_reconstruct_stripes on their own device stripes with fresh erasure
+pattern cache -- rs_decode (host API), rs_decode_batch, rs_encode,
+rs_encode_batch and rs_reconstruct_stripes on their own device stripes with fresh erasure
 patterns -- with a small pattern cap (RSMI_PATTERN_CAP) so the cache is
 evicted over and over while other threads read it.  Every result is checked
 (host API against the input, device stripes against a clone).  Prints one
@@ -43,7 +43,7 @@ def main():
     f = rsmi.FEC(k, n)
     P = ctypes.c_void_p
     stop = time.time() + a.seconds
-    counts = {"decode": 0, "decode_batch": 0, "encode": 0, "reconstruct_stripes": 0}
+    counts = {"decode": 0, "decode_batch": 0, "encode": 0, "reconstruct_stripes": 0, "encode_batch": 0}
     failures = []
     lock = threading.Lock()
 
@@ -73,7 +73,7 @@ def main():
         local = dict.fromkeys(counts, 0)
         it = 0
         while time.time() < stop:
-            op = it % 4
+            op = it % 5
             it += 1
             try:
                 if op == 0:
@@ -100,11 +100,19 @@ def main():
                     st = (ctypes.c_int * B)()
                     assert lib.rs_decode_batch(f.handle, B, cnts, nums, ptrs, S, dsts, st) == 0
                     assert list(st) == [0] * B and all(np.array_equal(o, blob) for o in outs)
+                elif op == 4:
+                    B = 6
+                    pars = [np.zeros(m * S, dtype=np.uint8) for _ in range(B)]
+                    ins = (ctypes.c_void_p * B)(*[blob.ctypes.data] * B)
+                    outs = (ctypes.c_void_p * B)(*[x.ctypes.data for x in pars])
+                    st = (ctypes.c_int * B)()
+                    assert lib.rs_encode_batch(f.handle, B, ins, k * S, outs, st) == 0
+                    assert list(st) == [0] * B and all(np.array_equal(x, par) for x in pars)
                 elif op == 2:
                     p2 = np.zeros(m * S, dtype=np.uint8)
                     assert lib.rs_encode(f.handle, P(blob.ctypes.data), k * S, P(p2.ctypes.data)) == 0
                     assert np.array_equal(p2, par)
-                else:
+                elif op == 3:
                     er = np.zeros((stripes, n), dtype=np.uint8)
                     for s in range(stripes):
                         er[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 1
