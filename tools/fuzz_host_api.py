@@ -92,8 +92,12 @@ def run(seconds=None, cases=None, seed=1):
     stats = {"cases": 0, "encode": 0, "decode_k": 0, "decode_more": 0, "corrupted": 0, "arena": 0,
              "pinned_dst": 0, "encode_batch_msgs": 0, "decode_batch_msgs": 0, "failures": 0}
     first = []
-    t0 = time.time()
+    t0 = last_note = time.time()
     while (cases is None or stats["cases"] < cases) and (seconds is None or time.time() - t0 < seconds):
+        if time.time() - last_note > 30:  # progress on stderr: a long run is seen to be alive
+            last_note = time.time()
+            print(f"fuzz_host_api: {stats['cases']} cases, {stats['failures']} failures, {last_note - t0:.0f} s",
+                  file=sys.stderr, flush=True)
         k, n = CODES[int(rng.integers(0, len(CODES)))]
         m = n - k
         if (k, n) not in fecs:

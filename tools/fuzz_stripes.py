@@ -35,7 +35,11 @@ def main():
     t0 = time.time()
     cases = fails = 0
     first = []
+    last_note = t0
     while time.time() - t0 < a.seconds:
+        if time.time() - last_note > 30:  # progress on stderr: a long run is seen to be alive
+            last_note = time.time()
+            print(f"fuzz_stripes: {cases} cases, {fails} failures, {last_note - t0:.0f} s", file=sys.stderr, flush=True)
         k, n = codes[int(rng.integers(0, len(codes)))]
         m = n - k
         # half the contexts keep small calls on the bit-sliced kernels
