@@ -115,8 +115,11 @@ int rs_decode(rs_ctx *ctx, int *numbers, const uint8_t **shares, int count,
  * status[b] (rs_decode's codes; each message's slice of numbers/shares is
  * sorted in place).  Messages with more than k distinct shares take the
  * rs_decode path (Correct); the rest are staged through pinned memory and
- * regenerated by one rs_reconstruct_stripes launch.  Returns RS_OK if every
- * message decoded, else the first failing status. */
+ * regenerated by rs_reconstruct_stripes launches that read the survivors over
+ * PCIe where they lie (engine-pinned) or where they were staged, in chunks.
+ * Batches beyond the pinned-staging cap (512 MiB; RSMI_BATCH_STAGE_MB) go in
+ * groups of messages.  Returns RS_OK if every message decoded, else the first
+ * failing status (in message order). */
 int rs_decode_batch(rs_ctx *ctx, int batch, const int *counts, int *numbers,
                     const uint8_t **shares, size_t share_len, uint8_t **dsts, int *status);
 
@@ -127,8 +130,9 @@ int rs_decode_batch(rs_ctx *ctx, int batch, const int *counts, int *numbers,
  * receives (n - k) * len / k bytes laid out as rs_encode's parity.  The
  * messages are staged through pinned memory in chunks (the staging copy of
  * one chunk overlaps the kernel of the previous one, which reads and writes
- * the staging over PCIe).  status[b] gets each message's code; returns RS_OK
- * if every message encoded, else the first failing status. */
+ * the staging over PCIe), in groups of messages within the pinned-staging cap
+ * (512 MiB; RSMI_BATCH_STAGE_MB).  status[b] gets each message's code;
+ * returns RS_OK if every message encoded, else the first failing status. */
 int rs_encode_batch(rs_ctx *ctx, int batch, const uint8_t *const *inputs, size_t len,
                     uint8_t *const *parities, int *status);
 
@@ -190,7 +194,7 @@ enum {
     RS_STAT_DECODES_IN_PLACE = 6,  /* rs_decode calls that read engine-pinned survivors in place */
     RS_STAT_REC_STRIPES_TABLE = 7,  /* stripes reconstructed by the split-table kernel (batched API) */
     RS_STAT_REC_STRIPES_SYNDROME = 8, /* ... by the bit-sliced syndrome kernels                     */
-    RS_STAT_ENCODE_BATCHES = 9,    /* rs_encode_batch calls coded in batched GPU passes */
+    RS_STAT_ENCODE_BATCHES = 9,    /* rs_encode_batch GPU passes (one per staging group) */
 };
 int64_t rs_stat(const rs_ctx *ctx, int which);
 

@@ -1928,11 +1928,47 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     return rebuild_into(c, *lg.L, present, by_id, share_len, dst);
 }
 
+namespace {
+// Pinned staging one batched host-API pass may use (rs_encode_batch: inputs +
+// parity; rs_decode_batch: survivors + regenerated rows).  Larger batches go
+// in groups of messages, so a lease's pinned memory stays bounded whatever the
+// batch (RSMI_BATCH_STAGE_MB overrides, for tests).
+size_t batch_stage_cap() {
+    static const size_t cap = [] {
+        const char* e = std::getenv("RSMI_BATCH_STAGE_MB");
+        const long v = e ? std::atol(e) : 0;
+        return (v > 0 ? static_cast<size_t>(v) : size_t(512)) << 20;
+    }();
+    return cap;
+}
+}  // namespace
+
 int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const uint8_t** shares,
                     size_t S, uint8_t** dsts, int* status) {
     if (!c || batch < 0 || (batch && (!counts || !numbers || !shares || !dsts || !status)))
         return RS_EINVAL;
     const int k = c->k, n = c->n;
+    {
+        // Groups of messages within the staging cap (k survivors and at most
+        // k regenerated rows each), in message order; the first failing
+        // status of the whole batch is returned.
+        const size_t per_msg = 2 * static_cast<size_t>(k) * round_up(std::max<size_t>(S, 1), 256);
+        const size_t group = std::max<size_t>(1, batch_stage_cap() / per_msg);
+        if (static_cast<size_t>(batch) > group) {
+            int rc = RS_OK;
+            size_t off = 0;
+            for (int b0 = 0; b0 < batch;) {
+                const int nb = static_cast<int>(std::min<size_t>(group, static_cast<size_t>(batch - b0)));
+                size_t cnt = 0;
+                for (int b = b0; b < b0 + nb; ++b) cnt += static_cast<size_t>(std::max(counts[b], 0));
+                const int r = rs_decode_batch(c, nb, counts + b0, numbers + off, shares + off, S, dsts + b0, status + b0);
+                if (r != RS_OK && rc == RS_OK) rc = r;
+                off += cnt;
+                b0 += nb;
+            }
+            return rc;
+        }
+    }
     // 1. validate + sort each message (rs_decode semantics); messages with
     //    exactly k distinct shares go to the batched launch.
     std::vector<size_t> first(batch + 1, 0);
@@ -2202,10 +2238,6 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     return fin != RS_OK ? fin : rc;
 }
 
-// Pinned staging one rs_encode_batch group may use (inputs + parity); larger
-// batches go in groups, and a message that alone exceeds it takes rs_encode.
-constexpr size_t kEncBatchStage = size_t(512) << 20;
-
 int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t len, uint8_t* const* parities,
                     int* status) {
     if (!c || batch < 0 || (batch && (!inputs || !parities || !status))) return RS_EINVAL;
@@ -2232,7 +2264,7 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
     // pinned staging followed by [group][m][pitch] of parity.
     const size_t pitch = round_up(S, 64);
     const size_t per_msg = (k + m) * pitch;
-    if (per_msg > kEncBatchStage || round_up(S, 16) / 16 >= (size_t(1) << 28)) {
+    if (per_msg > batch_stage_cap() || round_up(S, 16) / 16 >= (size_t(1) << 28)) {
         for (int b : todo) {
             status[b] = rs_encode(c, inputs[b], len, parities[b]);
             if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
@@ -2247,7 +2279,7 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
     rsmi::HostPipeline* pipe = L.pipeline();
     if (!pipe) return RS_ENOMEM;
     const hipStream_t s = L.stream;
-    const size_t group = std::max<size_t>(1, kEncBatchStage / per_msg);
+    const size_t group = std::max<size_t>(1, batch_stage_cap() / per_msg);
     for (size_t g0 = 0; g0 < todo.size(); g0 += group) {
         const size_t B = std::min(group, todo.size() - g0);
         if (!L.st_batch.acquire(B * per_msg)) return RS_ENOMEM;
@@ -2294,8 +2326,8 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
             for (size_t j = g0; j < todo.size(); ++j) status[todo[j]] = RS_EDEVICE;
             return RS_EDEVICE;
         }
+        c->encode_batches += 1;  // one per batched GPU pass (group)
     }
-    c->encode_batches += 1;
     return rc;
 }
 

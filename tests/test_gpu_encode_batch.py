@@ -125,3 +125,42 @@ def test_encode_batch_messages_alias_nothing_between_calls():
         assert st == [0] * 24
         assert par[rep] == oracle.encode(E, k, n, msgs[rep])
         assert par[-1] == oracle.encode(E, k, n, msgs[-1])
+
+
+def test_batches_split_into_staging_groups():
+    """A batch larger than the pinned-staging cap goes in groups of messages
+    (both batch calls; RSMI_BATCH_STAGE_MB=2 in a child process): every
+    message still matches the oracle, and rs_decode_batch returns the first
+    failing status in message order across groups."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys; sys.path[:0] = ['.', 'noise-erasurecode-plugin_amd']
+import numpy as np, rsmi
+from oracle import oracle
+k, n, S, B = 10, 14, 8192, 40
+f = rsmi.NewFEC(k, n); E = oracle.fec_matrix(k, n)
+msgs = [oracle.splitmix_bytes(k * S, 300 + b).tobytes() for b in range(B)]
+b0 = f.stat(f.STAT_ENCODE_BATCHES)
+par, st = f.EncodeBatch(msgs)
+assert st == [0] * B
+assert all(par[b] == oracle.encode(E, k, n, msgs[b]) for b in range(B))
+assert f.stat(f.STAT_ENCODE_BATCHES) - b0 >= 2, "one group only"
+rng = np.random.default_rng(9); batch = []
+for b in range(B):
+    sh = [msgs[b][i*S:(i+1)*S] for i in range(k)] + [par[b][i*S:(i+1)*S] for i in range(n - k)]
+    keep = rng.choice(n, size=k, replace=False).tolist()
+    batch.append([rsmi.Share(i, sh[i]) for i in keep])
+batch[33] = batch[33][:k - 1]       # not enough shares, in a later group
+s0 = f.stat(f.STAT_BATCHES_STAGED)
+outs, st = f.DecodeBatch(batch)
+assert st[33] == rsmi.RS_ENOT_ENOUGH and outs[33] is None
+assert all(st[b] == 0 and outs[b] == msgs[b] for b in range(B) if b != 33)
+assert f.stat(f.STAT_BATCHES_STAGED) - s0 >= 3, "one group only"
+print('ok')
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, RSMI_BATCH_STAGE_MB="2"))
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout, r.stderr[-2000:])
