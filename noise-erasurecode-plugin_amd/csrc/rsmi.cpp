@@ -2355,6 +2355,25 @@ int rs_blake2b_batch(rs_ctx* c, int count, const uint8_t* const* msgs, const siz
     if (!msgs || !lens || !out) return RS_EINVAL;
     for (int i = 0; i < count; ++i)
         if (!msgs[i] && lens[i]) return RS_EINVAL;
+    {
+        // Consecutive groups of messages within the pinned-staging cap (a
+        // message alone may exceed it: it is one group by itself).
+        size_t total = 0;
+        for (int i = 0; i < count; ++i) total += round_up(lens[i], 16);
+        if (count > 1 && total > batch_stage_cap()) {
+            for (int i0 = 0; i0 < count;) {
+                int i1 = i0;
+                size_t bytes = 0;
+                while (i1 < count && (i1 == i0 || bytes + round_up(lens[i1], 16) <= batch_stage_cap()))
+                    bytes += round_up(lens[i1++], 16);
+                const int r = rs_blake2b_batch(c, i1 - i0, msgs + i0, lens + i0, digest_len,
+                                               out + static_cast<size_t>(i0) * digest_len);
+                if (r != RS_OK) return r;
+                i0 = i1;
+            }
+            return RS_OK;
+        }
+    }
     // Longest messages first: the quads of one wave then run about the same
     // number of blocks.  Messages are packed 16-byte aligned in that order.
     std::vector<uint32_t> order(count);

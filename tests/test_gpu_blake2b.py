@@ -115,6 +115,29 @@ def test_blake2b_batch_of_large_messages_chunked():
     assert all(g == hashlib.blake2b(m, digest_size=32).digest() for m, g in zip(msgs, got))
 
 
+def test_blake2b_batch_split_into_staging_groups():
+    """Beyond the pinned-staging cap (RSMI_BATCH_STAGE_MB=1, a child
+    process) the batch is hashed in groups of consecutive messages, one of
+    them larger than the cap by itself; every digest matches hashlib."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, hashlib; sys.path[:0] = ['.', 'noise-erasurecode-plugin_amd']
+import numpy as np, rsmi
+from oracle import oracle
+f = rsmi.NewFEC(10, 14)
+lens = [300 << 10] * 6 + [3 << 20] + [1000, 0, 700 << 10] * 3
+msgs = [oracle.splitmix_bytes(n, 40 + i).tobytes() for i, n in enumerate(lens)]
+got = f.blake2b_batch(msgs, 32)
+assert all(g == hashlib.blake2b(m, digest_size=32).digest() for m, g in zip(msgs, got))
+print('ok')
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, RSMI_BATCH_STAGE_MB="1"))
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
 def test_blake2b_bad_arguments():
     lib = rsmi.load()
     import ctypes
