@@ -67,7 +67,7 @@ def test_prof_line_roles_and_traffic(tmp_path):
     md = out.read_text()
     rows = {line.split("|")[1].strip(): line for line in md.splitlines() if line.startswith("| ")}
     assert "2 | 10.000" in rows["headline encode"] and "2 | 9.000" in rows["headline reconstruct"]
-    assert "| 2 |" in rows["config1 (one message per launch)"]
+    assert "| 2 |" in rows["config1 (host-API launches: single messages and batches)"]
     assert "config5 encode" in rows and "config5 reconstruct" in rows
     # encode traffic per launch: (5e6 x 2 + 4e6) KiB = 14.336 GB
     assert json.loads(traffic.read_text()) == {"encode_k10_n14_S1048576_stripes1": 14.336}

@@ -8,8 +8,9 @@ config1 + config5 legs; tools/gpu/r04*.sh layout):
 Launches are told apart by kernel and grid size:
   headline   rs_matmul_kernel launches with the largest grid, in launch order
              alternating encode / reconstruct (bench.py --mode both);
-  config1    the other rs_matmul_kernel launches (one 1,048,580-byte message
-             per launch: 10 x 104,858-byte shards);
+  config1    the other rs_matmul_kernel launches (the host-API calls on
+             1,048,580-byte messages: one message per launch, and the
+             encode / decode batches' chunk launches);
   config5    rs_bitslice_k64_m16 (encode) and rs_bitslice_rec_k64_m16
              (reconstruct), invert_patterns_kernel (the fresh patterns).
 HBM traffic per launch = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 (the gfx950
@@ -56,7 +57,7 @@ def roles(trace):
     big = max((grid(r) for r in mm), default=0)
     head = [r for r in mm if grid(r) == big]
     out = {"headline encode": head[0::2], "headline reconstruct": head[1::2],
-           "config1 (one message per launch)": [r for r in mm if grid(r) != big],
+           "config1 (host-API launches: single messages and batches)": [r for r in mm if grid(r) != big],
            "config5 encode": [r for r in trace if "rs_bitslice_k64_m16" in r["Kernel_Name"]],
            "config5 reconstruct": [r for r in trace if "rs_bitslice_rec_k64_m16" in r["Kernel_Name"]],
            "pattern builds": [r for r in trace if "invert_patterns_kernel" in r["Kernel_Name"]]}
@@ -88,7 +89,7 @@ def main():
     # algorithmic bytes per launch
     alg = {"headline encode": 6553 * 14 * (1 << 20),
            "headline reconstruct": 6553 * (10 + 2.5) * (1 << 20),   # E[e] = 2.5 for 1..4 uniform
-           "config1 (one message per launch)": None,
+           "config1 (host-API launches: single messages and batches)": None,
            "config5 encode": 16384 * 80 * 65536,
            "config5 reconstruct": 16384 * (64 + 8.5) * 65536}       # E[e] = 8.5 for 1..16 uniform
     if b and "config" in b:
