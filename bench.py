@@ -98,12 +98,14 @@ def parse():
                     help="seconds after which a stuck gather leg is abandoned (the line is still printed, "
                          f"then the ranks exit {EXIT_GATHER_ABANDONED})")
     ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
-                    help="N = 1: skip the configs[0] (per-message latency) and configs[4] (RS(64,16)) "
-                         "legs reported beside the headline")
+                    help="N = 1: skip the configs[0] (per-message latency), configs[4] (RS(64,16)) and "
+                         "configs[2] worst-case legs reported beside the headline")
     ap.add_argument("--config1-reps", type=int, default=50)
     ap.add_argument("--config5-stripes", type=int, default=16384)
     ap.add_argument("--config5-steps", type=int, default=5)
     ap.add_argument("--config5-warmup", type=int, default=2)
+    ap.add_argument("--config3-steps", type=int, default=3,
+                    help="N = 1: steps of the configs[2] worst-case leg (4 data erasures in every stripe; 0 skips)")
     return ap.parse_args()
 
 
@@ -585,6 +587,33 @@ def config1_leg(local, reps=50):
     }
 
 
+def config3_worst_leg(local, dev, stripes, S, steps=3, warmup=1):
+    """configs[2]'s worst case: RS(10,4) with the same
+    four data shards (0-3) erased in every stripe, so every stripe
+    regenerates 4 data shards from 6 data + 4 parity survivors -- the most
+    arithmetic a reconstruct does and the encode's byte count (k + 4 shards
+    per stripe).  Reconstruct only (parity encoded once, untimed), HIP
+    events, GB/s on the algorithmic bytes."""
+    import rsmi
+    k, n = 10, 14
+    f = rsmi.FEC(k, n, device=local)
+    fixed = np.zeros((stripes, n), dtype=np.uint8)
+    fixed[:, [0, 1, 2, 3]] = 1
+    run = device_run(f, k, n, S, stripes, steps, warmup, [fixed] * (warmup + steps), False, True, dev,
+                     prepare_emax=4)
+    rec_bytes = stripes * (k + 4) * S
+    rec_ms = sum(run["reconstruct_ms"]) / steps
+    gbps = rec_bytes / (rec_ms / 1e3) / 1e9
+    return {
+        "status": "ok",
+        "what": f"configs[2] worst case: RS(10,4), {stripes} stripes x 10 x {S} B, data shards 0-3 erased in "
+                "every stripe (4 regenerated from 6 data + 4 parity)",
+        "steps": steps, "warmup": warmup, "stripes": stripes, "shard_bytes": S,
+        "reconstruct": {"kernel": f.kernel_name(1), "ms": round(rec_ms, 3), "GBps": round(gbps, 1),
+                        "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes": rec_bytes},
+    }
+
+
 def config5_leg(local, dev, stripes=16384, steps=5, warmup=2):
     """configs[4]: the wide code RS(64,16) with 64 KiB shards, `stripes`
     stripes (64 x 64 KiB = 4 MiB of data each) device-resident, a fresh
@@ -780,6 +809,8 @@ def main():
         out["config1"] = guarded_leg(lambda: config1_leg(local, args.config1_reps))
         out["config5"] = guarded_leg(lambda: config5_leg(local, dev, args.config5_stripes, args.config5_steps,
                                                          args.config5_warmup))
+        if args.config3_steps > 0:
+            out["config3_worst"] = guarded_leg(lambda: config3_worst_leg(local, dev, stripes, S, args.config3_steps))
     if rank == 0:
         emit(out)
     if distributed:

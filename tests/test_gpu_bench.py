@@ -57,7 +57,8 @@ def test_bench_two_ranks_gloo_with_gather_leg(torch_dev):
 @pytest.mark.gpu
 def test_bench_single_gpu_extra_legs(torch_dev):
     d = _run(["--stripes", "64", "--shard", "65536", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.2",
-              "--config1-reps", "3", "--config5-stripes", "64", "--config5-steps", "2", "--config5-warmup", "1"])
+              "--config1-reps", "3", "--config5-stripes", "64", "--config5-steps", "2", "--config5-warmup", "1",
+              "--config3-steps", "2"])
     assert d["n_gpus"] == 1 and d["roofline"]["frac"] > 0
     assert d["cpu_baseline"] and d["cpu_baseline"]["value"] > 0
     c1 = d["config1"]
@@ -71,3 +72,6 @@ def test_bench_single_gpu_extra_legs(torch_dev):
     assert c5["status"] == "ok", c5
     assert c5["encode"]["GBps"] > 0 and c5["reconstruct"]["GBps"] > 0
     assert c5["encode"]["bytes"] == 64 * 80 * 65536
+    c3 = d["config3_worst"]
+    assert c3["status"] == "ok", c3
+    assert c3["reconstruct"]["bytes"] == 64 * 14 * 65536 and c3["reconstruct"]["GBps"] > 0
