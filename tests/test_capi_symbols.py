@@ -50,3 +50,23 @@ def test_strerror_and_no_gpu_behaviour():
         with pytest.raises(rsmi.RSError) as ei:
             rsmi.NewFEC(10, 14)
         assert ei.value.code == rsmi.RS_EDEVICE
+
+
+def test_null_context_is_rejected_without_a_device():
+    """Every host-API entry point that takes a context refuses a NULL one
+    with RS_EINVAL before touching HIP (the cgo shim may pass a nil *FEC's
+    context); callable on a CPU-only machine."""
+    import ctypes
+    import rsmi
+    lib = rsmi.load()
+    i32 = ctypes.c_int
+    st = (i32 * 1)()
+    ptrs = (ctypes.c_void_p * 1)(None)
+    nums = (i32 * 1)(0)
+    lens = (ctypes.c_size_t * 1)(0)
+    out = ctypes.create_string_buffer(64)
+    assert lib.rs_encode(None, None, 0, None) == rsmi.RS_EINVAL
+    assert lib.rs_encode_batch(None, 1, ptrs, 10, ptrs, st) == rsmi.RS_EINVAL
+    assert lib.rs_decode_batch(None, 1, nums, nums, ptrs, 10, ptrs, st) == rsmi.RS_EINVAL
+    assert lib.rs_decode(None, nums, ptrs, 1, 10, out) == rsmi.RS_EINVAL
+    assert lib.rs_blake2b_batch(None, 1, ptrs, lens, 32, out) == rsmi.RS_EINVAL
