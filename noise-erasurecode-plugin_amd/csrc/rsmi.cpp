@@ -2022,220 +2022,232 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
     }
     if (fast.empty()) return rc;
-    // 3. the rest: one pointer-mode reconstruct launch.  PCIe carries only
-    //    the k survivors of each message in (packed [batch][k][pitch]) and
-    //    only the regenerated data shards out; the kernel reads survivors
-    //    where they landed and writes each erased shard to its own row of an
-    //    output buffer (data rows first), through a [batch][n] shard-address
-    //    table.  Present data shards go from the caller's buffers to dst on
-    //    the host.
-    const size_t pitch = round_up(S, 256);
-    const size_t B = fast.size();
-    std::vector<uint8_t> erased(B * static_cast<size_t>(n), 0);
-    std::vector<rsmi::CopyPool::Piece> in, direct;
-    std::vector<uint8_t*> regen;  // output row r (< E) -> caller destination
-    size_t n_par_out = 0;
-    for (size_t j = 0; j < B; ++j)
-        for (int i = 0; i < n; ++i) {
-            const uint8_t* p = by[fast[j]][i];
-            if (p) {
-                if (i < k) direct.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, p, S});
-            } else {
-                erased[j * n + i] = 1;
-                if (i < k) regen.push_back(dsts[fast[j]] + static_cast<size_t>(i) * S);
-                else ++n_par_out;
+    auto fast_path = [&]() -> int {
+        // 3. the rest: one pointer-mode reconstruct launch.  PCIe carries only
+        //    the k survivors of each message in (packed [batch][k][pitch]) and
+        //    only the regenerated data shards out; the kernel reads survivors
+        //    where they landed and writes each erased shard to its own row of an
+        //    output buffer (data rows first), through a [batch][n] shard-address
+        //    table.  Present data shards go from the caller's buffers to dst on
+        //    the host.
+        const size_t pitch = round_up(S, 256);
+        const size_t B = fast.size();
+        std::vector<uint8_t> erased(B * static_cast<size_t>(n), 0);
+        std::vector<rsmi::CopyPool::Piece> in, direct;
+        std::vector<uint8_t*> regen;  // output row r (< E) -> caller destination
+        size_t n_par_out = 0;
+        for (size_t j = 0; j < B; ++j)
+            for (int i = 0; i < n; ++i) {
+                const uint8_t* p = by[fast[j]][i];
+                if (p) {
+                    if (i < k) direct.push_back({dsts[fast[j]] + static_cast<size_t>(i) * S, p, S});
+                } else {
+                    erased[j * n + i] = 1;
+                    if (i < k) regen.push_back(dsts[fast[j]] + static_cast<size_t>(i) * S);
+                    else ++n_par_out;
+                }
             }
+        const size_t E = regen.size();
+        const size_t out_rows = E + n_par_out;
+        // Zero-copy receive: when every survivor lies, 16-byte aligned, in
+        // engine-pinned memory (rs_pinned_alloc / rs_arena), the kernel reads it
+        // there over PCIe -- no staging copy, no H2D of survivors.
+        const size_t sb = round_up(S, 16);
+        std::vector<uint64_t> dev_of(B * static_cast<size_t>(n), 0);
+        bool in_place = std::getenv("RSMI_NO_DIRECT") == nullptr;
+        for (size_t j = 0; j < B && in_place; ++j)
+            for (int i = 0; i < n && in_place; ++i)
+                if (const uint8_t* p = by[fast[j]][i]) {
+                    const uint64_t d = (reinterpret_cast<uintptr_t>(p) & 15u) ? 0 : rsmi::pinned_device_address(p, sb);
+                    in_place = d != 0;
+                    dev_of[j * n + i] = d;
+                }
+        const size_t packed = in_place ? 0 : B * static_cast<size_t>(k) * pitch;
+        ++(in_place ? c->batches_in_place : c->batches_staged);
+        DeviceGuard g(c->device);
+        if (!g.ok) return RS_EDEVICE;
+        LeaseGuard lg(c);
+        if (!lg.L) return RS_ENOMEM;
+        Lease& L = *lg.L;
+        rsmi::HostPipeline* pipe = L.pipeline();
+        if (!pipe) return RS_ENOMEM;
+        const hipStream_t s = L.stream;
+        static const bool batch_dma = [] {
+            const char* e = std::getenv("RSMI_BATCH_DMA");  // 1: stage survivors by DMA (round 4; A/B)
+            return e && std::atoi(e) != 0;
+        }();
+        if (!batch_dma) {
+            // Survivors read by the kernel over PCIe where they are (engine-pinned,
+            // in_place) or where the copy pool staged them (non-temporal stores),
+            // in chunks of messages: chunk i is reconstructed while chunk i + 1
+            // is staged and chunk i - 1's regenerated data shards -- written by
+            // the kernel into pinned staging -- are copied out; erased parity (not
+            // returned) goes to a device scratch row.  No DMA: the round-4 form
+            // queued every chunk's H2D, then the kernel, then the D2H
+            // (RSMI_BATCH_DMA=1).
+            const size_t sp = round_up(S, 64);
+            const size_t in_bytes = in_place ? 0 : B * static_cast<size_t>(k) * sp;
+            const size_t tbl = B * static_cast<size_t>(n) * sizeof(uint64_t);
+            if (!L.st_batch.acquire(in_bytes + std::max<size_t>(E, 1) * sp) || !L.st_pieces.acquire(tbl) ||
+                !L.d_pieces.reserve_on(tbl, s) || !L.d_batch.reserve_on(std::max<size_t>(n_par_out, 1) * sp, s))
+                return RS_ENOMEM;
+            uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
+            uint8_t* hd = static_cast<uint8_t*>(L.st_batch.dev);
+            uint8_t* h_out = h + in_bytes;
+            uint8_t* d_out = hd + in_bytes;
+            uint8_t* d_par = static_cast<uint8_t*>(L.d_batch.p);
+            uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
+            std::vector<rsmi::CopyPool::Piece> stage_in;
+            stage_in.reserve(B * static_cast<size_t>(k));
+            size_t r_data = 0, r_par = 0;
+            for (size_t j = 0; j < B; ++j) {
+                size_t q = 0;
+                for (int i = 0; i < n; ++i) {
+                    uint64_t& t = tab[j * n + i];
+                    if (const uint8_t* p = by[fast[j]][i]) {
+                        const size_t slot = j * k + q++;
+                        if (in_place) {
+                            t = dev_of[j * n + i];
+                        } else {
+                            stage_in.push_back({h + slot * sp, p, S, true});
+                            t = reinterpret_cast<uint64_t>(hd + slot * sp);
+                        }
+                    } else if (i < k) {
+                        t = reinterpret_cast<uint64_t>(d_out + r_data++ * sp);
+                    } else {
+                        t = reinterpret_cast<uint64_t>(d_par + r_par++ * sp);
+                    }
+                }
+            }
+            auto finish = [&](int code) {
+                if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
+                return code;
+            };
+            L.begin(s);
+            if (hipMemcpyAsync(L.d_pieces.p, tab, tbl, hipMemcpyHostToDevice, s) != hipSuccess) return finish(RS_EDEVICE);
+            L.st_pieces.release_after(s);
+            const size_t moved = B * static_cast<size_t>(k) * sp;  // survivor bytes the kernels read
+            const size_t nch = std::min<size_t>(B, moved >= kBatchChunkMin ? kBatchChunks : 1);
+            std::vector<size_t> rows_before(B + 1, 0);  // regenerated data rows of messages [0, j)
+            for (size_t j = 0; j < B; ++j) {
+                size_t e_j = 0;
+                for (int i = 0; i < k; ++i) e_j += by[fast[j]][i] == nullptr;
+                rows_before[j + 1] = rows_before[j] + e_j;
+            }
+            size_t launched = 0;
+            for (size_t ch = 0; ch < nch; ++ch) {
+                const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+                if (!in_place)
+                    pipe->copy(std::vector<rsmi::CopyPool::Piece>(stage_in.begin() + j0 * k, stage_in.begin() + j1 * k));
+                const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, sp, S, j1 - j0, erased.data() + j0 * n,
+                                           static_cast<const uint64_t*>(L.d_pieces.p) + j0 * n, s);
+                if (st != RS_OK || hipEventRecord(L.ev[ch], s) != hipSuccess) return finish(st != RS_OK ? st : RS_EDEVICE);
+                ++launched;
+            }
+            pipe->copy(direct);  // present data shards: no GPU, while it works
+            for (size_t ch = 0; ch < launched; ++ch) {
+                if (rsmi::wait_event(L.ev[ch]) != hipSuccess) return finish(RS_EDEVICE);
+                const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+                std::vector<rsmi::CopyPool::Piece> out;
+                for (size_t r = rows_before[j0]; r < rows_before[j1]; ++r) out.push_back({regen[r], h_out + r * sp, S});
+                pipe->copy(out);
+            }
+            return RS_OK;
         }
-    const size_t E = regen.size();
-    const size_t out_rows = E + n_par_out;
-    // Zero-copy receive: when every survivor lies, 16-byte aligned, in
-    // engine-pinned memory (rs_pinned_alloc / rs_arena), the kernel reads it
-    // there over PCIe -- no staging copy, no H2D of survivors.
-    const size_t sb = round_up(S, 16);
-    std::vector<uint64_t> dev_of(B * static_cast<size_t>(n), 0);
-    bool in_place = std::getenv("RSMI_NO_DIRECT") == nullptr;
-    for (size_t j = 0; j < B && in_place; ++j)
-        for (int i = 0; i < n && in_place; ++i)
-            if (const uint8_t* p = by[fast[j]][i]) {
-                const uint64_t d = (reinterpret_cast<uintptr_t>(p) & 15u) ? 0 : rsmi::pinned_device_address(p, sb);
-                in_place = d != 0;
-                dev_of[j * n + i] = d;
-            }
-    const size_t packed = in_place ? 0 : B * static_cast<size_t>(k) * pitch;
-    ++(in_place ? c->batches_in_place : c->batches_staged);
-    DeviceGuard g(c->device);
-    if (!g.ok) return RS_EDEVICE;
-    LeaseGuard lg(c);
-    if (!lg.L) return RS_ENOMEM;
-    Lease& L = *lg.L;
-    rsmi::HostPipeline* pipe = L.pipeline();
-    if (!pipe) return RS_ENOMEM;
-    const hipStream_t s = L.stream;
-    static const bool batch_dma = [] {
-        const char* e = std::getenv("RSMI_BATCH_DMA");  // 1: stage survivors by DMA (round 4; A/B)
-        return e && std::atoi(e) != 0;
-    }();
-    if (!batch_dma) {
-        // Survivors read by the kernel over PCIe where they are (engine-pinned,
-        // in_place) or where the copy pool staged them (non-temporal stores),
-        // in chunks of messages: chunk i is reconstructed while chunk i + 1
-        // is staged and chunk i - 1's regenerated data shards -- written by
-        // the kernel into pinned staging -- are copied out; erased parity (not
-        // returned) goes to a device scratch row.  No DMA: the round-4 form
-        // queued every chunk's H2D, then the kernel, then the D2H
-        // (RSMI_BATCH_DMA=1).
-        const size_t sp = round_up(S, 64);
-        const size_t in_bytes = in_place ? 0 : B * static_cast<size_t>(k) * sp;
-        const size_t tbl = B * static_cast<size_t>(n) * sizeof(uint64_t);
-        if (!L.st_batch.acquire(in_bytes + std::max<size_t>(E, 1) * sp) || !L.st_pieces.acquire(tbl) ||
-            !L.d_pieces.reserve_on(tbl, s) || !L.d_batch.reserve_on(std::max<size_t>(n_par_out, 1) * sp, s))
+        L.begin(s);  // the lease's buffers may last have been read on another stream
+        const size_t table_bytes = B * static_cast<size_t>(n) * sizeof(uint64_t);
+        if (!L.st_batch.acquire(std::max<size_t>(std::max(packed, E * pitch), 16)) ||
+            (packed && !L.d_pack.reserve_on(packed, s)) || !L.d_batch.reserve_on(std::max<size_t>(out_rows, 1) * pitch, s) ||
+            !L.st_pieces.acquire(table_bytes) || !L.d_pieces.reserve_on(table_bytes, s))
             return RS_ENOMEM;
+        // From the first async copy on, every exit waits for the stream: the
+        // staging buffers may not be reused (or freed) while a DMA reads them.
+        auto finish = [&](int code) {
+            if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
+            L.end(s);
+            return code;
+        };
         uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
-        uint8_t* hd = static_cast<uint8_t*>(L.st_batch.dev);
-        uint8_t* h_out = h + in_bytes;
-        uint8_t* d_out = hd + in_bytes;
-        uint8_t* d_par = static_cast<uint8_t*>(L.d_batch.p);
+        uint8_t* dp = static_cast<uint8_t*>(L.d_pack.p);
+        uint8_t* dout = static_cast<uint8_t*>(L.d_batch.p);
         uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
-        std::vector<rsmi::CopyPool::Piece> stage_in;
-        stage_in.reserve(B * static_cast<size_t>(k));
-        size_t r_data = 0, r_par = 0;
+        size_t r_data = 0, r_par = E;
         for (size_t j = 0; j < B; ++j) {
             size_t q = 0;
             for (int i = 0; i < n; ++i) {
                 uint64_t& t = tab[j * n + i];
                 if (const uint8_t* p = by[fast[j]][i]) {
-                    const size_t slot = j * k + q++;
+                    const size_t slot = j * k + q++;  // exactly k present (fast path)
                     if (in_place) {
                         t = dev_of[j * n + i];
                     } else {
-                        stage_in.push_back({h + slot * sp, p, S, true});
-                        t = reinterpret_cast<uint64_t>(hd + slot * sp);
+                        in.push_back({h + slot * pitch, p, S});
+                        t = reinterpret_cast<uint64_t>(dp + slot * pitch);
                     }
-                } else if (i < k) {
-                    t = reinterpret_cast<uint64_t>(d_out + r_data++ * sp);
                 } else {
-                    t = reinterpret_cast<uint64_t>(d_par + r_par++ * sp);
+                    t = reinterpret_cast<uint64_t>(dout + (i < k ? r_data++ : r_par++) * pitch);
                 }
             }
         }
-        auto finish = [&](int code) {
-            if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
-            return code;
-        };
-        L.begin(s);
-        if (hipMemcpyAsync(L.d_pieces.p, tab, tbl, hipMemcpyHostToDevice, s) != hipSuccess) return finish(RS_EDEVICE);
+        if (hipMemcpyAsync(L.d_pieces.p, tab, table_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+            return finish(RS_EDEVICE);
         L.st_pieces.release_after(s);
-        const size_t moved = B * static_cast<size_t>(k) * sp;  // survivor bytes the kernels read
-        const size_t nch = std::min<size_t>(B, moved >= kBatchChunkMin ? kBatchChunks : 1);
-        std::vector<size_t> rows_before(B + 1, 0);  // regenerated data rows of messages [0, j)
-        for (size_t j = 0; j < B; ++j) {
-            size_t e_j = 0;
-            for (int i = 0; i < k; ++i) e_j += by[fast[j]][i] == nullptr;
-            rows_before[j + 1] = rows_before[j] + e_j;
+        // Staged survivors go in chunks of messages: the host staging copy of
+        // chunk i + 1 runs while chunk i crosses PCIe (the staging buffer is
+        // pinned, so each hipMemcpyAsync returns at once).  `in` holds exactly k
+        // pieces per message, in message order.
+        const size_t chunks = in_place ? 0 : std::min<size_t>(B, packed >= kBatchChunkMin ? kBatchChunks : 1);
+        for (size_t ch = 0; ch < chunks; ++ch) {
+            const size_t j0 = B * ch / chunks, j1 = B * (ch + 1) / chunks;
+            pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
+            if (hipMemcpyAsync(dp + j0 * k * pitch, h + j0 * k * pitch, (j1 - j0) * k * pitch, hipMemcpyHostToDevice, s) !=
+                hipSuccess)
+                return finish(RS_EDEVICE);
         }
-        size_t launched = 0;
-        for (size_t ch = 0; ch < nch; ++ch) {
-            const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
-            if (!in_place)
-                pipe->copy(std::vector<rsmi::CopyPool::Piece>(stage_in.begin() + j0 * k, stage_in.begin() + j1 * k));
-            const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, sp, S, j1 - j0, erased.data() + j0 * n,
-                                       static_cast<const uint64_t*>(L.d_pieces.p) + j0 * n, s);
-            if (st != RS_OK || hipEventRecord(L.ev[ch], s) != hipSuccess) return finish(st != RS_OK ? st : RS_EDEVICE);
-            ++launched;
+        const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, pitch, S, B, erased.data(),
+                                   static_cast<const uint64_t*>(L.d_pieces.p), s);
+        if (st != RS_OK) return finish(st);
+        // Regenerated data shards out, in chunks with an event each, so the host
+        // copies chunk i into the callers' buffers while chunk i + 1 crosses.
+        // (The D2H reuses the survivor staging: the stream orders it after the
+        // H2D copies that read it.)
+        const size_t ochunks = E == 0 ? 0 : std::min<size_t>(E, E * pitch >= kBatchChunkMin ? kBatchChunks : 1);
+        int rc_dev = RS_OK;
+        size_t queued = 0;
+        for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch, ++queued) {
+            const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
+            if (hipMemcpyAsync(h + r0 * pitch, dout + r0 * pitch, (r1 - r0) * pitch, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess ||
+                hipEventRecord(L.ev[ch], s) != hipSuccess)
+                rc_dev = RS_EDEVICE;
         }
-        pipe->copy(direct);  // present data shards: no GPU, while it works
-        for (size_t ch = 0; ch < launched; ++ch) {
-            if (rsmi::wait_event(L.ev[ch]) != hipSuccess) return finish(RS_EDEVICE);
-            const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
+        // present data shards need no GPU: copy them while the GPU works
+        if (rc_dev == RS_OK) pipe->copy(direct);
+        for (size_t ch = 0; ch < queued && rc_dev == RS_OK; ++ch) {
+            const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
+            if (hipEventSynchronize(L.ev[ch]) != hipSuccess) {
+                rc_dev = RS_EDEVICE;
+                break;
+            }
             std::vector<rsmi::CopyPool::Piece> out;
-            for (size_t r = rows_before[j0]; r < rows_before[j1]; ++r) out.push_back({regen[r], h_out + r * sp, S});
+            out.reserve(r1 - r0);
+            for (size_t r = r0; r < r1; ++r) out.push_back({regen[r], h + r * pitch, S});
             pipe->copy(out);
         }
-        return rc;
-    }
-    L.begin(s);  // the lease's buffers may last have been read on another stream
-    const size_t table_bytes = B * static_cast<size_t>(n) * sizeof(uint64_t);
-    if (!L.st_batch.acquire(std::max<size_t>(std::max(packed, E * pitch), 16)) ||
-        (packed && !L.d_pack.reserve_on(packed, s)) || !L.d_batch.reserve_on(std::max<size_t>(out_rows, 1) * pitch, s) ||
-        !L.st_pieces.acquire(table_bytes) || !L.d_pieces.reserve_on(table_bytes, s))
-        return RS_ENOMEM;
-    // From the first async copy on, every exit waits for the stream: the
-    // staging buffers may not be reused (or freed) while a DMA reads them.
-    auto finish = [&](int code) {
-        if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
-        L.end(s);
-        return code;
+        const int fin = finish(rc_dev);
+        L.st_batch.release_after(s);
+        return fin;
     };
-    uint8_t* h = static_cast<uint8_t*>(L.st_batch.p);
-    uint8_t* dp = static_cast<uint8_t*>(L.d_pack.p);
-    uint8_t* dout = static_cast<uint8_t*>(L.d_batch.p);
-    uint64_t* tab = static_cast<uint64_t*>(L.st_pieces.p);
-    size_t r_data = 0, r_par = E;
-    for (size_t j = 0; j < B; ++j) {
-        size_t q = 0;
-        for (int i = 0; i < n; ++i) {
-            uint64_t& t = tab[j * n + i];
-            if (const uint8_t* p = by[fast[j]][i]) {
-                const size_t slot = j * k + q++;  // exactly k present (fast path)
-                if (in_place) {
-                    t = dev_of[j * n + i];
-                } else {
-                    in.push_back({h + slot * pitch, p, S});
-                    t = reinterpret_cast<uint64_t>(dp + slot * pitch);
-                }
-            } else {
-                t = reinterpret_cast<uint64_t>(dout + (i < k ? r_data++ : r_par++) * pitch);
-            }
-        }
-    }
-    if (hipMemcpyAsync(L.d_pieces.p, tab, table_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-        return finish(RS_EDEVICE);
-    L.st_pieces.release_after(s);
-    // Staged survivors go in chunks of messages: the host staging copy of
-    // chunk i + 1 runs while chunk i crosses PCIe (the staging buffer is
-    // pinned, so each hipMemcpyAsync returns at once).  `in` holds exactly k
-    // pieces per message, in message order.
-    const size_t chunks = in_place ? 0 : std::min<size_t>(B, packed >= kBatchChunkMin ? kBatchChunks : 1);
-    for (size_t ch = 0; ch < chunks; ++ch) {
-        const size_t j0 = B * ch / chunks, j1 = B * (ch + 1) / chunks;
-        pipe->copy(std::vector<rsmi::CopyPool::Piece>(in.begin() + j0 * k, in.begin() + j1 * k));
-        if (hipMemcpyAsync(dp + j0 * k * pitch, h + j0 * k * pitch, (j1 - j0) * k * pitch, hipMemcpyHostToDevice, s) !=
-            hipSuccess)
-            return finish(RS_EDEVICE);
-    }
-    const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, pitch, S, B, erased.data(),
-                               static_cast<const uint64_t*>(L.d_pieces.p), s);
-    if (st != RS_OK) return finish(st);
-    // Regenerated data shards out, in chunks with an event each, so the host
-    // copies chunk i into the callers' buffers while chunk i + 1 crosses.
-    // (The D2H reuses the survivor staging: the stream orders it after the
-    // H2D copies that read it.)
-    const size_t ochunks = E == 0 ? 0 : std::min<size_t>(E, E * pitch >= kBatchChunkMin ? kBatchChunks : 1);
-    int rc_dev = RS_OK;
-    size_t queued = 0;
-    for (size_t ch = 0; ch < ochunks && rc_dev == RS_OK; ++ch, ++queued) {
-        const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
-        if (hipMemcpyAsync(h + r0 * pitch, dout + r0 * pitch, (r1 - r0) * pitch, hipMemcpyDeviceToHost, s) !=
-                hipSuccess ||
-            hipEventRecord(L.ev[ch], s) != hipSuccess)
-            rc_dev = RS_EDEVICE;
-    }
-    // present data shards need no GPU: copy them while the GPU works
-    if (rc_dev == RS_OK) pipe->copy(direct);
-    for (size_t ch = 0; ch < queued && rc_dev == RS_OK; ++ch) {
-        const size_t r0 = E * ch / ochunks, r1 = E * (ch + 1) / ochunks;
-        if (hipEventSynchronize(L.ev[ch]) != hipSuccess) {
-            rc_dev = RS_EDEVICE;
-            break;
-        }
-        std::vector<rsmi::CopyPool::Piece> out;
-        out.reserve(r1 - r0);
-        for (size_t r = r0; r < r1; ++r) out.push_back({regen[r], h + r * pitch, S});
-        pipe->copy(out);
-    }
-    const int fin = finish(rc_dev);
-    L.st_batch.release_after(s);
-    return fin != RS_OK ? fin : rc;
+    // A failure of the batched pass fails every message it carried (their
+    // outputs were not all produced); the call returns the first failing
+    // status in message order.
+    const int fr = fast_path();
+    if (fr != RS_OK)
+        for (int b : fast) status[b] = fr;
+    (void)rc;
+    for (int b = 0; b < batch; ++b)
+        if (status[b] != RS_OK) return status[b];
+    return RS_OK;
 }
 
 int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t len, uint8_t* const* parities,
@@ -2271,18 +2283,25 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
         }
         return rc;
     }
+    // A message not coded gets the call's failure (never a stale RS_OK).
+    auto fail_from = [&](size_t j0, int code) {
+        for (size_t j = j0; j < todo.size(); ++j) status[todo[j]] = code;
+        for (int b = 0; b < batch; ++b)
+            if (status[b] != RS_OK) return status[b];
+        return code;
+    };
     DeviceGuard g(c->device);
-    if (!g.ok) return RS_EDEVICE;
+    if (!g.ok) return fail_from(0, RS_EDEVICE);
     LeaseGuard lg(c);
-    if (!lg.L) return RS_ENOMEM;
+    if (!lg.L) return fail_from(0, RS_ENOMEM);
     Lease& L = *lg.L;
     rsmi::HostPipeline* pipe = L.pipeline();
-    if (!pipe) return RS_ENOMEM;
+    if (!pipe) return fail_from(0, RS_ENOMEM);
     const hipStream_t s = L.stream;
     const size_t group = std::max<size_t>(1, batch_stage_cap() / per_msg);
     for (size_t g0 = 0; g0 < todo.size(); g0 += group) {
         const size_t B = std::min(group, todo.size() - g0);
-        if (!L.st_batch.acquire(B * per_msg)) return RS_ENOMEM;
+        if (!L.st_batch.acquire(B * per_msg)) return fail_from(g0, RS_ENOMEM);
         uint8_t* h_in = static_cast<uint8_t*>(L.st_batch.p);
         uint8_t* h_out = h_in + B * k * pitch;
         uint8_t* d_in = static_cast<uint8_t*>(L.st_batch.dev);
@@ -2324,11 +2343,14 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
         if (e != hipSuccess) {
             (void)hipStreamSynchronize(s);  // nothing may still read the staging
             for (size_t j = g0; j < todo.size(); ++j) status[todo[j]] = RS_EDEVICE;
-            return RS_EDEVICE;
+            break;
         }
         c->encode_batches += 1;  // one per batched GPU pass (group)
     }
-    return rc;
+    (void)rc;
+    for (int b = 0; b < batch; ++b)  // the first failing status in message order
+        if (status[b] != RS_OK) return status[b];
+    return RS_OK;
 }
 
 int rs_blake2b_device(rs_ctx* c, int count, const uint64_t* msg_ptrs, const uint64_t* lens, const uint32_t* order,

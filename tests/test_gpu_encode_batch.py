@@ -164,3 +164,35 @@ print('ok')
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=180,
                        env=dict(os.environ, RSMI_BATCH_STAGE_MB="2"))
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+def test_decode_batch_failure_marks_its_messages():
+    """A failing batched pass (the context's first pattern build made to fail,
+    RSMI_TEST_FAIL_FLUSH=1) fails every message it carried -- none keeps a
+    stale RS_OK -- while a Correct-path message in the same call decodes;
+    the next call on the context decodes everything."""
+    import os
+    k, n, S = 10, 14, 4096
+    old = os.environ.get("RSMI_TEST_FAIL_FLUSH")
+    os.environ["RSMI_TEST_FAIL_FLUSH"] = "1"
+    try:
+        f = rsmi.FEC(k, n)
+    finally:
+        if old is None:
+            del os.environ["RSMI_TEST_FAIL_FLUSH"]
+        else:
+            os.environ["RSMI_TEST_FAIL_FLUSH"] = old
+    E = oracle.fec_matrix(k, n)
+    msgs = _messages(k, S, 6, 77)
+    batch = []
+    for b, data in enumerate(msgs):
+        par = oracle.encode(E, k, n, data)
+        sh = [data[i * S:(i + 1) * S] for i in range(k)] + [par[i * S:(i + 1) * S] for i in range(n - k)]
+        keep = [i for i in range(n) if i != b % k][: k + (2 if b == 2 else 0)]  # message 2: Correct path
+        batch.append([rsmi.Share(i, sh[i]) for i in keep])
+    outs, st = f.DecodeBatch(batch)
+    assert st[2] == 0 and outs[2] == msgs[2]
+    assert all(st[b] != 0 and outs[b] is None for b in range(6) if b != 2), st
+    outs, st = f.DecodeBatch(batch)
+    assert st == [0] * 6 and outs == msgs
+    f.close()
