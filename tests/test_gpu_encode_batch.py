@@ -196,3 +196,36 @@ def test_decode_batch_failure_marks_its_messages():
     outs, st = f.DecodeBatch(batch)
     assert st == [0] * 6 and outs == msgs
     f.close()
+
+
+@pytest.mark.parametrize("nt", ["1", "0"])
+def test_staging_copy_modes_match_oracle(nt):
+    """Small staged messages (rs_encode / rs_decode, both staging chunks) and
+    a batch, with the non-temporal staging copy (default) and with memcpy
+    (RSMI_STAGE_NT=0; the knob is read once per process: a child)."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys; sys.path[:0] = ['.', 'noise-erasurecode-plugin_amd']
+import numpy as np, rsmi
+from oracle import oracle
+k, n = 10, 14
+f = rsmi.NewFEC(k, n); E = oracle.fec_matrix(k, n)
+for S in (1, 4095, 104858, 65543):
+    data = oracle.splitmix_bytes(k * S, S).tobytes()
+    par = f.encode_parity(data)
+    assert par == oracle.encode(E, k, n, data), S
+    sh = [data[i*S:(i+1)*S] for i in range(k)] + [par[i*S:(i+1)*S] for i in range(n - k)]
+    keep = [13, 2, 11, 4, 5, 6, 10, 8, 9, 12]
+    got = f.Decode(None, [rsmi.Share(i, sh[i]) for i in keep])
+    assert got == data, S
+msgs = [oracle.splitmix_bytes(k * 70001, 9 + b).tobytes() for b in range(30)]
+pars, st = f.EncodeBatch(msgs)
+assert st == [0] * 30 and all(p == oracle.encode(E, k, n, m) for p, m in zip(pars, msgs))
+print('ok')
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, RSMI_STAGE_NT=nt))
+    assert r.returncode == 0 and "ok" in r.stdout, (nt, r.stdout, r.stderr[-2000:])
