@@ -60,6 +60,26 @@ PYBIND11_MODULE(_rsmi_host, m) {
                  check(f.Encode(reinterpret_cast<const uint8_t*>(s.data()), s.size(),
                                 [&](const ShareView& v) { output(v.DeepCopy()); }));
              })
+        .def("EncodeBatch",
+             [](FEC& f, const std::vector<py::bytes>& inputs) {
+                 // equal-length messages (rs_encode_batch); None where a message failed
+                 std::vector<std::string> keep(inputs.begin(), inputs.end());
+                 std::vector<const uint8_t*> ptrs;
+                 for (const std::string& x : keep) ptrs.push_back(reinterpret_cast<const uint8_t*>(x.data()));
+                 const size_t len = keep.empty() ? 0 : keep[0].size();
+                 for (const std::string& x : keep)
+                     if (x.size() != len) throw std::invalid_argument("EncodeBatch: messages of unequal length");
+                 std::vector<std::vector<uint8_t>> par;
+                 std::vector<Status> st;
+                 {
+                     py::gil_scoped_release nogil;
+                     f.EncodeBatch(ptrs, len, &par, &st);
+                 }
+                 py::list res;
+                 for (size_t b = 0; b < par.size(); ++b)
+                     res.append(st[b].ok() ? py::object(to_bytes(par[b])) : py::object(py::none()));
+                 return res;
+             })
         .def("DecodeBatch",
              [](FEC& f, std::vector<std::vector<Share>> msgs) {
                  std::vector<std::vector<uint8_t>> outs;

@@ -432,6 +432,20 @@ def test_prepare_shards_batch_matches_single():
     assert p.HashBytes([b"abc"]) == [hashlib.blake2b(b"abc", digest_size=32).digest()]
 
 
+def test_host_fec_encode_batch():
+    """The C++ host layer's FEC::EncodeBatch (pybind): every message's
+    parity equals the oracle's; a length that is not a multiple of k gives
+    None for every message."""
+    k, n = 10, 14
+    f = h.NewFEC(k, n)
+    E = oracle.fec_matrix(k, n)
+    msgs = [oracle.splitmix_bytes(10 * 6007, 40 + b).tobytes() for b in range(9)]
+    got = f.EncodeBatch(msgs)
+    assert got == [oracle.encode(E, k, n, m) for m in msgs]
+    assert f.EncodeBatch([b"x" * 13, b"y" * 13]) == [None, None]
+    assert f.EncodeBatch([]) == []
+
+
 def test_prepare_shards_batch_equal_lengths_one_pass():
     """Equal-length inputs are encoded in one rs_encode_batch pass per length
     (send-side batching): every message's Shards equal prepareShards' and
