@@ -2277,11 +2277,10 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
     const size_t pitch = round_up(S, 64);
     const size_t per_msg = (k + m) * pitch;
     if (per_msg > batch_stage_cap() || round_up(S, 16) / 16 >= (size_t(1) << 28)) {
-        for (int b : todo) {
-            status[b] = rs_encode(c, inputs[b], len, parities[b]);
-            if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
-        }
-        return rc;
+        for (int b : todo) status[b] = rs_encode(c, inputs[b], len, parities[b]);
+        for (int b = 0; b < batch; ++b)  // the first failing status in message order
+            if (status[b] != RS_OK) return status[b];
+        return RS_OK;
     }
     // A message not coded gets the call's failure (never a stale RS_OK).
     auto fail_from = [&](size_t j0, int code) {
