@@ -2021,7 +2021,13 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
         status[b] = rs_decode(c, numbers + first[b], shares + first[b], counts[b], S, dsts[b]);
         if (status[b] != RS_OK && rc == RS_OK) rc = status[b];
     }
-    if (fast.empty()) return rc;
+    auto first_fail = [&] {  // the call's result: the first failing status in message order
+        for (int b = 0; b < batch; ++b)
+            if (status[b] != RS_OK) return status[b];
+        return static_cast<int>(RS_OK);
+    };
+    (void)rc;
+    if (fast.empty()) return first_fail();
     auto fast_path = [&]() -> int {
         // 3. the rest: one pointer-mode reconstruct launch.  PCIe carries only
         //    the k survivors of each message in (packed [batch][k][pitch]) and
@@ -2244,10 +2250,7 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     const int fr = fast_path();
     if (fr != RS_OK)
         for (int b : fast) status[b] = fr;
-    (void)rc;
-    for (int b = 0; b < batch; ++b)
-        if (status[b] != RS_OK) return status[b];
-    return RS_OK;
+    return first_fail();
 }
 
 int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t len, uint8_t* const* parities,
