@@ -1941,6 +1941,15 @@ size_t batch_stage_cap() {
     }();
     return cap;
 }
+
+// Chunks of messages for the direct batch forms: one per 256 KiB of input
+// bytes, at most kBatchChunks (their events) and one message each at least
+// -- two config-1 messages already run as two chunks, the first coded while
+// the second is staged (the single-message path's two-chunk overlap).
+size_t direct_batch_chunks(size_t messages, size_t in_bytes) {
+    const size_t by_bytes = std::max<size_t>(1, in_bytes / (size_t(256) << 10));
+    return std::max<size_t>(1, std::min({messages, kBatchChunks, by_bytes}));
+}
 }  // namespace
 
 int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const uint8_t** shares,
@@ -2028,6 +2037,11 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
     };
     (void)rc;
     if (fast.empty()) return first_fail();
+    if (fast.size() == 1) {  // one message: the single-message path (two staged column chunks)
+        const int b = fast[0];
+        status[b] = rs_decode(c, numbers + first[b], shares + first[b], counts[b], S, dsts[b]);
+        return first_fail();
+    }
     auto fast_path = [&]() -> int {
         // 3. the rest: one pointer-mode reconstruct launch.  PCIe carries only
         //    the k survivors of each message in (packed [batch][k][pitch]) and
@@ -2133,7 +2147,7 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
             if (hipMemcpyAsync(L.d_pieces.p, tab, tbl, hipMemcpyHostToDevice, s) != hipSuccess) return finish(RS_EDEVICE);
             L.st_pieces.release_after(s);
             const size_t moved = B * static_cast<size_t>(k) * sp;  // survivor bytes the kernels read
-            const size_t nch = std::min<size_t>(B, moved >= kBatchChunkMin ? kBatchChunks : 1);
+            const size_t nch = direct_batch_chunks(B, moved);
             std::vector<size_t> rows_before(B + 1, 0);  // regenerated data rows of messages [0, j)
             for (size_t j = 0; j < B; ++j) {
                 size_t e_j = 0;
@@ -2279,7 +2293,9 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
     // pinned staging followed by [group][m][pitch] of parity.
     const size_t pitch = round_up(S, 64);
     const size_t per_msg = (k + m) * pitch;
-    if (per_msg > batch_stage_cap() || round_up(S, 16) / 16 >= (size_t(1) << 28)) {
+    // One message (it gets rs_encode's two-chunk staged path) or messages past
+    // the staging cap / the kernels' column range: one rs_encode each.
+    if (todo.size() == 1 || per_msg > batch_stage_cap() || round_up(S, 16) / 16 >= (size_t(1) << 28)) {
         for (int b : todo) status[b] = rs_encode(c, inputs[b], len, parities[b]);
         for (int b = 0; b < batch; ++b)  // the first failing status in message order
             if (status[b] != RS_OK) return status[b];
@@ -2312,7 +2328,7 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
         // Chunks of messages: the staging copy of chunk i + 1 (copy pool,
         // non-temporal) runs while the kernel codes chunk i over PCIe, and
         // chunk i's parity is copied out while chunk i + 1's kernel runs.
-        const size_t nch = std::min<size_t>(B, B * k * pitch >= kBatchChunkMin ? kBatchChunks : 1);
+        const size_t nch = direct_batch_chunks(B, B * k * pitch);
         hipError_t e = hipSuccess;
         size_t launched = 0;
         for (size_t ch = 0; ch < nch && e == hipSuccess; ++ch) {
