@@ -229,3 +229,29 @@ print('ok')
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=180,
                        env=dict(os.environ, RSMI_STAGE_NT=nt))
     assert r.returncode == 0 and "ok" in r.stdout, (nt, r.stdout, r.stderr[-2000:])
+
+
+def test_one_message_batches_take_the_single_message_path():
+    """A batch of one message is coded by rs_encode / rs_decode's two-chunk
+    staged path (no batched pass counted), bit-exact; two messages already
+    go through the batched pass."""
+    k, n, S = 10, 14, 104858
+    f = fec(k, n)
+    E = oracle.fec_matrix(k, n)
+    msgs = _messages(k, S, 2, 4242)
+    b0 = f.stat(rsmi.FEC.STAT_ENCODE_BATCHES)
+    par, st = f.EncodeBatch(msgs[:1])
+    assert st == [0] and par[0] == oracle.encode(E, k, n, msgs[0])
+    assert f.stat(rsmi.FEC.STAT_ENCODE_BATCHES) == b0
+    par2, st = f.EncodeBatch(msgs)
+    assert st == [0, 0] and par2[1] == oracle.encode(E, k, n, msgs[1])
+    assert f.stat(rsmi.FEC.STAT_ENCODE_BATCHES) == b0 + 1
+    s0 = f.stat(rsmi.FEC.STAT_BATCHES_STAGED)
+    batch = []
+    for data, p in zip(msgs, par2):
+        sh = [data[i * S:(i + 1) * S] for i in range(k)] + [p[i * S:(i + 1) * S] for i in range(n - k)]
+        batch.append([rsmi.Share(i, sh[i]) for i in (13, 1, 12, 3, 4, 11, 6, 7, 8, 10)])
+    outs, st = f.DecodeBatch(batch[:1])
+    assert st == [0] and outs == msgs[:1] and f.stat(rsmi.FEC.STAT_BATCHES_STAGED) == s0
+    outs, st = f.DecodeBatch(batch)
+    assert st == [0, 0] and outs == msgs and f.stat(rsmi.FEC.STAT_BATCHES_STAGED) == s0 + 1
