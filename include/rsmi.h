@@ -273,6 +273,76 @@ int rs_device_alloc(rs_ctx *ctx, size_t bytes, void **out);
 int rs_device_free(rs_ctx *ctx, void *p);
 int rs_stream_sync(rs_ctx *ctx, void *stream);
 
+/* ---- device sets: one context over several GPUs ---------------------------
+ * north_star: "stripes are independent, so they are partitioned across the 8
+ * GPUs of one node with no collectives on the encode path"; SURVEY.md §8e and
+ * §7.5 ("one host thread + stream per GPU").  The plugin process that loads
+ * this library (through the Go shim's NewFECOnDevices) uses every GPU of the
+ * node through one context:
+ *
+ * rs_new_devices builds a context over `count` HIP devices (devices[i];
+ * repeats allowed -- two members on one GPU).  Member i is an ordinary
+ * single-device context on devices[i] (rs_member; owned by the set, never
+ * freed by the caller) with one host worker thread of its own.  Peer access
+ * is enabled between every pair of distinct member devices that supports it.
+ * Every entry point above accepts a device-set context:
+ *  - rs_encode / rs_decode (one message) run on the member with the fewest
+ *    calls in flight (concurrent Receive goroutines spread over the GPUs);
+ *  - rs_encode_batch / rs_decode_batch split the messages into `count`
+ *    contiguous ranges (rs_partition), each range on its member's thread, all
+ *    members at once; per-message status and the return value as on one GPU;
+ *  - the device-resident calls (rs_encode_stripes, rs_reconstruct_stripes,
+ *    rs_reconstruct_ptrs, rs_fill_splitmix, rs_blake2b_device) run on a
+ *    member on the device that holds their (first) device buffer, RS_EINVAL
+ *    if no member is on it; rs_prepare_patterns (stream must be NULL) runs
+ *    on every member; rs_blake2b* on the least-busy member;
+ *  - rs_stat / rs_pattern_count / rs_pattern_evictions are summed over the
+ *    members; rs_pattern_rows / rs_kernel_name / rs_device / rs_device_alloc
+ *    are member 0's.
+ * A single-device context is a set of one for the calls below. */
+int rs_new_devices(int k, int n, const int *devices, int count, rs_ctx **out);
+int rs_member_count(const rs_ctx *ctx);          /* 1 for a single-device context */
+rs_ctx *rs_member(rs_ctx *ctx, int i);           /* NULL if i is out of range    */
+
+/* Contiguous partition of `units` (stripes, messages) into `parts` ranges:
+ * part p covers [*first, *first + *count) with first = units*p/parts, so the
+ * ranges tile [0, units) in order and differ in size by at most one. */
+int rs_partition(size_t units, int parts, int part, size_t *first, size_t *count);
+
+/* Device-resident stripes already placed per member (stripe-local placement,
+ * the headline): part i describes the stripes member i holds, in that
+ * member's device memory, laid out as for rs_encode_stripes; stream is a
+ * stream of member i's device or NULL.  All members' launches are issued
+ * concurrently, one host thread per member; returns when every part is
+ * queued (RS_OK, or the first failing status in member order). */
+typedef struct rs_stripe_part {
+    void *data;
+    size_t data_stripe_stride;
+    void *parity;
+    size_t parity_stripe_stride;
+    size_t stripes;
+    void *stream;
+} rs_stripe_part;
+int rs_encode_stripes_parts(rs_ctx *ctx, const rs_stripe_part *parts, size_t shard_pitch, size_t shard_len);
+/* erased: HOST flags [sum of parts' stripes][n], in part order (part i's
+ * stripes follow part i-1's). */
+int rs_reconstruct_stripes_parts(rs_ctx *ctx, const rs_stripe_part *parts, size_t shard_pitch, size_t shard_len,
+                                 const uint8_t *erased);
+
+/* Shard-distributed placement (the device analogue of the
+ * plugin sending every shard to a different peer, main.go:207): shard i of
+ * stripe s lives on ANY member's device, at the device address
+ * shard_ptrs[s * n + i] (a HOST array; 16-byte aligned).  owner[s] (HOST) is
+ * the member that reconstructs stripe s: its kernel reads Rebuild's survivors
+ * where they lie -- over xGMI when they sit on another GPU (peer access, no
+ * staging copy, no collective) -- and writes each erased shard at its address
+ * (local or peer).  streams[i] (may be NULL, or hold NULLs) is member i's
+ * stream; the survivors must be complete when those streams run.  Returns
+ * when every member's launch is queued; RS_EDEVICE when the set spans devices
+ * without peer access. */
+int rs_reconstruct_spread(rs_ctx *ctx, const uint64_t *shard_ptrs, const int *owner, size_t shard_len,
+                          size_t stripes, const uint8_t *erased, void *const *streams);
+
 /* ---- bench / test utility (not on the codec path) ------------------------
  * Fill len bytes of device memory with the splitmix64 byte stream of seed
  * (byte i = byte i%8 of splitmix64(seed + (i/8 + 1) * golden)), the same

@@ -29,6 +29,7 @@
 
 #include "bitslice.hpp"
 #include "blake2b.hpp"
+#include "device_set.hpp"
 #include "gf256.hpp"
 #include "gf_invert.hpp"
 #include "host_pipeline.hpp"
@@ -268,6 +269,10 @@ struct Lease {
 struct rs_ctx {
     int k = 0, n = 0, m = 0, device = 0;
     std::vector<uint8_t> enc;  // n x k systematic matrix
+    // Device-set context (rs_new_devices): the members do all the work and
+    // every entry point forwards to them (device_set.hpp); nullptr for a
+    // single-device context, whose state is everything below.
+    rsmi::DeviceSet* set = nullptr;
     // Generated bit-sliced encode kernel for this (k, n), if one was built
     // and its embedded matrix equals enc (bitslice.hpp); nullptr otherwise.
     const rsmi::BitsliceKernel* bitslice = nullptr;
@@ -968,6 +973,64 @@ int reconstruct(rs_ctx* c, Lease& L, void* data, size_t dss, void* parity, size_
     return launch_reconstruct(c, L, data, dss, parity, pss, pitch, len, stripes, shard_ptrs, s);
 }
 
+// Pointer-mode reconstruct from a HOST table of shard addresses
+// [stripes][n] (rs_reconstruct_spread: one member's stripes): the table goes
+// through the lease's pinned staging into its device buffer on stream s,
+// then the reconstruct reads it like rs_reconstruct_ptrs' device table.
+int reconstruct_host_table(rs_ctx* c, const uint64_t* tab, size_t len, size_t stripes, const uint8_t* erased,
+                           hipStream_t s) {
+    const size_t bytes = stripes * static_cast<size_t>(c->n) * sizeof(uint64_t);
+    for (size_t i = 0; i < stripes * static_cast<size_t>(c->n); ++i)
+        if (tab[i] & 15u) return RS_EINVAL;  // the kernels move 16-byte vectors
+    DeviceGuard g(c->device);
+    if (!g.ok) return RS_EDEVICE;
+    LeaseGuard lg(c);
+    if (!lg.L) return RS_ENOMEM;
+    Lease& L = *lg.L;
+    L.begin(s);  // the lease's table buffer may last have been read on another stream
+    if (!L.st_pieces.acquire(bytes) || !L.d_pieces.reserve_on(bytes, s)) return RS_ENOMEM;
+    std::memcpy(L.st_pieces.p, tab, bytes);
+    const hipError_t e = hipMemcpyAsync(L.d_pieces.p, L.st_pieces.p, bytes, hipMemcpyHostToDevice, s);
+    L.st_pieces.release_after(s);
+    if (e != hipSuccess) {
+        L.end(s);
+        return RS_EDEVICE;
+    }
+    const int rc = reconstruct(c, L, nullptr, 0, nullptr, 0, round_up(len, 16), len, stripes, erased,
+                               static_cast<const uint64_t*>(L.d_pieces.p), s);
+    L.end(s);  // also when nothing was launched: the table copy wrote d_pieces on s
+    return rc;
+}
+
+// Holds the least busy member of a device set for one call.
+struct SetPick {
+    rsmi::DeviceSet* s;
+    int i;
+    explicit SetPick(rsmi::DeviceSet* set) : s(set), i(rsmi::set_acquire(set)) {}
+    ~SetPick() { rsmi::set_release(s, i); }
+    rs_ctx* member() const { return rsmi::set_member(s, i); }
+};
+
+// Member of a device set on the device holding p (nullptr: none).
+rs_ctx* routed(rs_ctx* c, const void* p) {
+    const int i = rsmi::set_route(c->set, p);
+    return i < 0 ? nullptr : rsmi::set_member(c->set, i);
+}
+
+// Member i of c (c itself for a single-device context, i == 0).
+rs_ctx* member_of(rs_ctx* c, int i) {
+    if (c->set) return rsmi::set_member(c->set, i);
+    return i == 0 ? c : nullptr;
+}
+
+int members_of(const rs_ctx* c) { return c->set ? rsmi::set_count(c->set) : 1; }
+
+// Runs job(i) for every member of c: concurrently for a set, inline for a
+// single-device context.
+int run_members(rs_ctx* c, const std::function<int(int)>& job) {
+    return c->set ? rsmi::set_run(c->set, job) : job(0);
+}
+
 // out_t = decode row (surv -> targets[t]) applied to the survivors, on the
 // GPU through L's pinned host pipeline.  Runs on c->device.
 int gpu_rows(rs_ctx* c, Lease& L, const std::vector<int>& surv, const std::vector<const uint8_t*>& surv_ptr,
@@ -1055,23 +1118,58 @@ bool encode_in_place(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_
     return true;
 }
 
-// Whether [dst, dst + len) meets any of the survivors by_id[surv[j]] (S bytes each).
-bool ranges_overlap(const uint8_t* dst, size_t len, const std::vector<const uint8_t*>& by_id,
-                    const std::vector<int>& surv, size_t S) {
-    const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst), d1 = d0 + len;
-    for (int id : surv) {
-        const uintptr_t s0 = reinterpret_cast<uintptr_t>(by_id[id]), s1 = s0 + S;
-        if (s0 < d1 && d0 < s1) return true;
+// Output ranges [start, end) of a decode call (one dst, or every dst of a
+// batch) and whether a share's S bytes meet any of them.
+class OutRanges {
+public:
+    void add(const uint8_t* p, size_t len) {
+        if (len) r_.push_back({reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + len});
     }
-    return false;
+    void seal() {  // sorted by start, with the running maximum of the ends
+        std::sort(r_.begin(), r_.end());
+        uintptr_t mx = 0;
+        for (auto& v : r_) v.second = mx = std::max(mx, v.second);
+    }
+    bool meets(const uint8_t* p, size_t S) const {
+        if (!S || r_.empty()) return false;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = a + S;
+        // the ranges starting before b; the largest end among them
+        auto it = std::lower_bound(r_.begin(), r_.end(), std::make_pair(b, uintptr_t(0)));
+        return it != r_.begin() && std::prev(it)->second > a;
+    }
+
+private:
+    std::vector<std::pair<uintptr_t, uintptr_t>> r_;
+};
+
+// infectious lets shares alias dst (Decode(dst, shares) with dst holding
+// received bytes).  The engine writes dst while its kernels still read the
+// survivors, and moves present shares within dst, so every share that meets
+// an output range is first copied aside (into `aside`) and its pointer in
+// by_id replaced (a copy-after-the-kernel rule alone missed
+// survivors stored in missing rows or one row below their own).  Returns the
+// number of shares set aside.
+size_t set_aside_aliases(const OutRanges& out, std::vector<const uint8_t*>& by_id, size_t S,
+                         std::vector<uint8_t>& aside) {
+    size_t cnt = 0;
+    for (const uint8_t* p : by_id) cnt += p && out.meets(p, S);
+    if (!cnt) return 0;
+    aside.resize(cnt * S);
+    size_t j = 0;
+    for (const uint8_t*& p : by_id)
+        if (p && out.meets(p, S)) {
+            std::memcpy(aside.data() + j * S, p, S);
+            p = aside.data() + j++ * S;
+        }
+    return cnt;
 }
 
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
 // Rebuild's choice `surv` is read at device address dev[j] (column chunk by
 // column chunk when nch > 1, `stage` filling each chunk's survivor columns
 // first); the present data shares are copied into dst (unless present_done)
-// while the kernel runs -- or after it, when dst overlaps a survivor the
-// kernel reads in place.  Returns kDecodeNoStaging, having done nothing, when
+// while the kernel runs (no share overlaps dst: rs_decode set aliasing ones
+// aside).  Returns kDecodeNoStaging, having done nothing, when
 // its pinned staging cannot be had (the caller falls back to the pipeline).
 using StageFn = std::function<void(size_t off, size_t w)>;
 constexpr int kDecodeNoStaging = -1000;
@@ -1173,10 +1271,8 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
         copy_present();
         return RS_OK;
     }
-    // A caller's dst may hold survivors (infectious lets shares alias dst):
-    // then the present shares are copied only after the kernel has read them
-    // (ADVICE r04).  Staged survivors (stage != null) are copies already.
-    const bool overlap = !stage && ranges_overlap(dst, static_cast<size_t>(k) * S, by_id, surv, S);
+    // dst never overlaps a share here: rs_decode sets aliasing shares aside
+    // (set_aside_aliases), so present shares go to dst while the kernel runs.
     std::vector<uint8_t> rows;
     if (!rsmi::decode_rows(c->enc, k, c->n, surv, missing, rows)) return RS_ESINGULAR;
     nch = std::max(1, std::min(nch, static_cast<int>(std::min<size_t>(kBatchChunks, S / 4096))));  // >= 4 KiB a chunk
@@ -1233,7 +1329,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
         if (err == hipSuccess) ++launched;
     }
     L.end(s);
-    if (!overlap) copy_present();  // while the kernel runs
+    copy_present();  // while the kernel runs
     for (int ch = 0; ch < launched; ++ch) {
         const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
         if (err == hipSuccess) err = w8;
@@ -1244,7 +1340,6 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                         static_cast<uint8_t*>(L.st_out.p) + t * span + off, w);
     }
     if (launched < nch) (void)rsmi::wait_event(L.dev_done);  // a failed launch: drain what was queued
-    if (overlap && err == hipSuccess) copy_present();
     return err == hipSuccess ? RS_OK : RS_EDEVICE;
 }
 
@@ -1315,13 +1410,7 @@ int rebuild_into(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
                 pieces.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
         rsmi::CopyPool::shared().run(pieces);
     };
-    // dst holding survivors: the pipeline stages them chunk by chunk while
-    // the overlap hook would run, so the copy waits for the GPU rows.
-    if (ranges_overlap(dst, static_cast<size_t>(k) * S, by_id, surv, S)) {
-        const int rc = gpu_rows(c, L, surv, sp, missing, outs, S);
-        if (rc == RS_OK) copy_present();
-        return rc;
-    }
+    // (dst overlaps no share: rs_decode set aliasing shares aside.)
     return gpu_rows(c, L, surv, sp, missing, outs, S, copy_present);
 }
 
@@ -1670,8 +1759,50 @@ int rs_new(int k, int n, rs_ctx** out) {
     return rs_new_on_device(k, n, dev, out);
 }
 
+int rs_new_devices(int k, int n, const int* devices, int count, rs_ctx** out) {
+    if (!out) return RS_EINVAL;
+    *out = nullptr;
+    if (k <= 0 || n <= 0 || k > 256 || n > 256 || k > n) return RS_EINVAL_KN;
+    if (!devices || count <= 0 || count > 256) return RS_EINVAL;
+    rs_ctx* c = new (std::nothrow) rs_ctx;
+    if (!c) return RS_ENOMEM;
+    c->k = k;
+    c->n = n;
+    c->m = n - k;
+    c->device = devices[0];
+    c->enc = rsmi::systematic_matrix(k, n);
+    const int st = rsmi::set_create(k, n, devices, count, &c->set);
+    if (st != RS_OK) {
+        delete c;
+        return st;
+    }
+    *out = c;
+    return RS_OK;
+}
+
+int rs_member_count(const rs_ctx* c) { return c ? members_of(c) : RS_EINVAL; }
+
+rs_ctx* rs_member(rs_ctx* c, int i) { return c ? member_of(c, i) : nullptr; }
+
+int rs_partition(size_t units, int parts, int part, size_t* first, size_t* count) {
+    if (parts <= 0 || part < 0 || part >= parts || !first || !count) return RS_EINVAL;
+    // units * part / parts without overflow for any size_t units
+    auto at = [&](size_t p) {
+        const size_t q = units / static_cast<size_t>(parts), r = units % static_cast<size_t>(parts);
+        return q * p + r * p / static_cast<size_t>(parts);
+    };
+    *first = at(static_cast<size_t>(part));
+    *count = at(static_cast<size_t>(part) + 1) - *first;
+    return RS_OK;
+}
+
 void rs_free(rs_ctx* c) {
     if (!c) return;
+    if (c->set) {
+        rsmi::set_destroy(c->set);
+        delete c;
+        return;
+    }
     {
         DeviceGuard g(c->device);
         (void)hipDeviceSynchronize();
@@ -1699,6 +1830,7 @@ int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
 
 const char* rs_kernel_name(const rs_ctx* c, int which) {
     if (!c) return "";
+    if (c->set) return rs_kernel_name(rsmi::set_member(c->set, 0), which);
     if (which == 0 && c->bitslice) return c->bitslice->name;
     if (which == 1 && use_bitslice_rec(c)) return c->rec_name.c_str();
     return rsmi::variant_name(c->k, c->m);
@@ -1706,18 +1838,37 @@ const char* rs_kernel_name(const rs_ctx* c, int which) {
 
 int rs_pattern_count(const rs_ctx* c) {
     if (!c) return RS_EINVAL;
+    if (c->set) {
+        int sum = 0;
+        for (int i = 0; i < rsmi::set_count(c->set); ++i) sum += rs_pattern_count(rsmi::set_member(c->set, i));
+        return sum;
+    }
     std::shared_lock<std::shared_mutex> rl(c->pat_mu);
     return static_cast<int>(c->pat_index.size());
 }
 
 int64_t rs_pattern_evictions(const rs_ctx* c) {
     if (!c) return RS_EINVAL;
+    if (c->set) {
+        int64_t sum = 0;
+        for (int i = 0; i < rsmi::set_count(c->set); ++i) sum += rs_pattern_evictions(rsmi::set_member(c->set, i));
+        return sum;
+    }
     std::shared_lock<std::shared_mutex> rl(c->pat_mu);
     return static_cast<int64_t>(c->evictions);
 }
 
 int64_t rs_stat(const rs_ctx* c, int which) {
     if (!c) return RS_EINVAL;
+    if (c->set) {
+        int64_t sum = 0;
+        for (int i = 0; i < rsmi::set_count(c->set); ++i) {
+            const int64_t v = rs_stat(rsmi::set_member(c->set, i), which);
+            if (v < 0) return v;
+            sum += v;
+        }
+        return sum;
+    }
     switch (which) {
         case RS_STAT_PATTERNS: return rs_pattern_count(c);
         case RS_STAT_EVICTIONS: return rs_pattern_evictions(c);
@@ -1738,6 +1889,7 @@ int64_t rs_stat(const rs_ctx* c, int which) {
 
 int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count) {
     if (!c || !erased || !rows || !count) return RS_EINVAL;
+    if (c->set) return rs_pattern_rows(rsmi::set_member(c->set, 0), erased, rows, count);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1764,6 +1916,10 @@ int rs_pattern_rows(rs_ctx* c, const uint8_t* erased, uint8_t* rows, int* count)
 
 int rs_prepare_patterns(rs_ctx* c, int max_e, void* stream) {
     if (!c || max_e < 0 || max_e > c->m) return RS_EINVAL;
+    if (c->set) {  // every member, each on its own device's null stream
+        if (stream) return RS_EINVAL;
+        return rsmi::set_run(c->set, [&](int i) { return rs_prepare_patterns(rsmi::set_member(c->set, i), max_e, nullptr); });
+    }
     // count = sum_{e=1..max_e} C(n, e)
     double total = 0, binom = 1;
     for (int e = 1; e <= max_e; ++e) {
@@ -1818,6 +1974,10 @@ int rs_encode_stripes(rs_ctx* c, const void* data, size_t dss, void* parity, siz
     if (!c) return RS_EINVAL;
     if (c->m == 0 || stripes == 0 || len == 0) return RS_OK;
     if (!check_stripes_args(c, data, dss, parity, pss, pitch, len)) return RS_EINVAL;
+    if (c->set) {
+        rs_ctx* mc = routed(c, data);
+        return mc ? rs_encode_stripes(mc, data, dss, parity, pss, pitch, len, stripes, stream) : RS_EINVAL;
+    }
     // Reads only state that is immutable after rs_new: no lock, no lease.
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
@@ -1833,6 +1993,10 @@ int rs_reconstruct_stripes(rs_ctx* c, void* data, size_t dss, void* parity, size
     if (!c || !erased) return RS_EINVAL;
     if (stripes == 0 || len == 0) return RS_OK;
     if (!check_stripes_args(c, data, dss, parity, pss, pitch, len)) return RS_EINVAL;
+    if (c->set) {
+        rs_ctx* mc = routed(c, data);
+        return mc ? rs_reconstruct_stripes(mc, data, dss, parity, pss, pitch, len, stripes, erased, stream) : RS_EINVAL;
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1847,6 +2011,10 @@ int rs_reconstruct_ptrs(rs_ctx* c, const uint64_t* shard_ptrs, size_t len, size_
     if (stripes == 0 || len == 0) return RS_OK;
     if (round_up(len, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;  // 32-bit column offsets
     if (reinterpret_cast<uintptr_t>(shard_ptrs) & 7u) return RS_EINVAL;
+    if (c->set) {
+        rs_ctx* mc = routed(c, shard_ptrs);
+        return mc ? rs_reconstruct_ptrs(mc, shard_ptrs, len, stripes, erased, stream) : RS_EINVAL;
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1861,6 +2029,10 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     const size_t S = len / static_cast<size_t>(c->k);
     if (S == 0 || c->m == 0) return RS_OK;
     if (!input || !parity) return RS_EINVAL;
+    if (c->set) {
+        const SetPick pk(c->set);
+        return rs_encode(pk.member(), input, len, parity);
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1916,6 +2088,17 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (share_len == 0) return RS_OK;
     for (int i = 0; i < n; ++i)
         if (present[i] && !by_id[i]) return RS_EINVAL;
+    if (c->set) {  // numbers / shares are sorted already: the member sorts them again as a no-op
+        const SetPick pk(c->set);
+        return rs_decode(pk.member(), numbers, shares, count, share_len, dst);
+    }
+    std::vector<uint8_t> aside;  // shares that alias dst, set aside before anything is written
+    {
+        OutRanges out;
+        out.add(dst, static_cast<size_t>(k) * share_len);
+        out.seal();
+        set_aside_aliases(out, by_id, share_len, aside);
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
@@ -1956,7 +2139,36 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
                     size_t S, uint8_t** dsts, int* status) {
     if (!c || batch < 0 || (batch && (!counts || !numbers || !shares || !dsts || !status)))
         return RS_EINVAL;
+    if (c->set) return rsmi::set_decode_batch(c->set, batch, counts, numbers, shares, S, dsts, status);
     const int k = c->k, n = c->n;
+    if (batch > 0 && S > 0) {
+        // Shares that alias any message's dst (infectious lets shares alias
+        // dst; a batch also lets message b's dst hold message b''s arena
+        // survivors): the present shares go to the dsts and regenerated rows
+        // come out while later chunks' kernels still read survivors, so those
+        // shares are copied aside first and the batch runs on a pointer array
+        // that names the copies; the caller's array is sorted like it.
+        size_t total = 0;
+        for (int b = 0; b < batch; ++b) total += static_cast<size_t>(std::max(counts[b], 0));
+        OutRanges out;
+        for (int b = 0; b < batch; ++b) out.add(dsts[b], static_cast<size_t>(k) * S);
+        out.seal();
+        std::vector<const uint8_t*> loc(shares, shares + total), orig(loc);
+        std::vector<uint8_t> aside;
+        if (set_aside_aliases(out, loc, S, aside)) {
+            const int rc = rs_decode_batch(c, batch, counts, numbers, loc.data(), S, dsts, status);
+            // loc was sorted with numbers; map copies back to the caller's pointers
+            const uintptr_t a0 = reinterpret_cast<uintptr_t>(aside.data()), a1 = a0 + aside.size();
+            std::vector<const uint8_t*> moved;  // orig pointers of the copies, in copy order
+            for (const uint8_t* p : orig)
+                if (p && out.meets(p, S)) moved.push_back(p);
+            for (size_t j = 0; j < total; ++j) {
+                const uintptr_t v = reinterpret_cast<uintptr_t>(loc[j]);
+                shares[j] = (v >= a0 && v < a1) ? moved[(v - a0) / S] : loc[j];
+            }
+            return rc;
+        }
+    }
     {
         // Groups of messages within the staging cap (k survivors and at most
         // k regenerated rows each), in message order; the first failing
@@ -2108,6 +2320,18 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
             const size_t sp = round_up(S, 64);
             const size_t in_bytes = in_place ? 0 : B * static_cast<size_t>(k) * sp;
             const size_t tbl = B * static_cast<size_t>(n) * sizeof(uint64_t);
+            // The lease's device buffers may last have been used on another
+            // stream: order s after that before reserve_on may free them
+            // (ADVICE r05), and release the staging after s on every exit.
+            L.begin(s);
+            struct StagingDone {
+                Lease& L;
+                hipStream_t s;
+                ~StagingDone() {
+                    L.st_batch.release_after(s);
+                    L.end(s);
+                }
+            } staging_done{L, s};
             if (!L.st_batch.acquire(in_bytes + std::max<size_t>(E, 1) * sp) || !L.st_pieces.acquire(tbl) ||
                 !L.d_pieces.reserve_on(tbl, s) || !L.d_batch.reserve_on(std::max<size_t>(n_par_out, 1) * sp, s))
                 return RS_ENOMEM;
@@ -2143,7 +2367,6 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
                 if (hipStreamSynchronize(s) != hipSuccess && code == RS_OK) code = RS_EDEVICE;
                 return code;
             };
-            L.begin(s);
             if (hipMemcpyAsync(L.d_pieces.p, tab, tbl, hipMemcpyHostToDevice, s) != hipSuccess) return finish(RS_EDEVICE);
             L.st_pieces.release_after(s);
             const size_t moved = B * static_cast<size_t>(k) * sp;  // survivor bytes the kernels read
@@ -2270,6 +2493,7 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
 int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t len, uint8_t* const* parities,
                     int* status) {
     if (!c || batch < 0 || (batch && (!inputs || !parities || !status))) return RS_EINVAL;
+    if (c->set) return rsmi::set_encode_batch(c->set, batch, inputs, len, parities, status);
     const size_t k = static_cast<size_t>(c->k), m = static_cast<size_t>(c->m);
     if (len % k != 0) {
         for (int b = 0; b < batch; ++b) status[b] = RS_ELEN_NOT_MULTIPLE;
@@ -2376,6 +2600,10 @@ int rs_blake2b_device(rs_ctx* c, int count, const uint64_t* msg_ptrs, const uint
     if (!c || count < 0 || digest_len < 1 || digest_len > 64) return RS_EINVAL;
     if (count == 0) return RS_OK;
     if (!msg_ptrs || !lens || !out) return RS_EINVAL;
+    if (c->set) {
+        rs_ctx* mc = routed(c, out);
+        return mc ? rs_blake2b_device(mc, count, msg_ptrs, lens, order, digest_len, out, stream) : RS_EINVAL;
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     rsmi::Blake2bArgs a{};
@@ -2395,6 +2623,10 @@ int rs_blake2b_batch(rs_ctx* c, int count, const uint8_t* const* msgs, const siz
     if (!msgs || !lens || !out) return RS_EINVAL;
     for (int i = 0; i < count; ++i)
         if (!msgs[i] && lens[i]) return RS_EINVAL;
+    if (c->set) {
+        const SetPick pk(c->set);
+        return rs_blake2b_batch(pk.member(), count, msgs, lens, digest_len, out);
+    }
     {
         // Consecutive groups of messages within the pinned-staging cap (a
         // message alone may exceed it: it is one group by itself).
@@ -2508,11 +2740,12 @@ int rs_blake2b(rs_ctx* c, int count, const uint8_t* const* msgs, const size_t* l
     const HashPlan hp = plan_hash(count, lens);
     if (hp.host) return rs_blake2b_host(count, msgs, lens, digest_len, out, hp.threads);
     if (where) *where = 1;
-    return rs_blake2b_batch(c, count, msgs, lens, digest_len, out);
+    return rs_blake2b_batch(c, count, msgs, lens, digest_len, out);  // a set picks its least busy member there
 }
 
 int rs_device_alloc(rs_ctx* c, size_t bytes, void** out) {
     if (!c || !out) return RS_EINVAL;
+    if (c->set) return rs_device_alloc(rsmi::set_member(c->set, 0), bytes, out);
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     return hipMalloc(out, bytes ? bytes : 1) == hipSuccess ? RS_OK : RS_ENOMEM;
@@ -2520,19 +2753,75 @@ int rs_device_alloc(rs_ctx* c, size_t bytes, void** out) {
 
 int rs_device_free(rs_ctx* c, void* p) {
     if (!c) return RS_EINVAL;
+    if (c->set) return rs_device_free(rsmi::set_member(c->set, 0), p);
     DeviceGuard g(c->device);
     return hip_status(hipFree(p));
 }
 
 int rs_stream_sync(rs_ctx* c, void* stream) {
     if (!c) return RS_EINVAL;
+    if (c->set) return rs_stream_sync(rsmi::set_member(c->set, 0), stream);
     DeviceGuard g(c->device);
     return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
+int rs_encode_stripes_parts(rs_ctx* c, const rs_stripe_part* parts, size_t pitch, size_t len) {
+    if (!c || !parts) return RS_EINVAL;
+    return run_members(c, [&](int i) -> int {
+        const rs_stripe_part& p = parts[i];
+        if (!p.stripes) return RS_OK;
+        return rs_encode_stripes(member_of(c, i), p.data, p.data_stripe_stride, p.parity, p.parity_stripe_stride, pitch,
+                                 len, p.stripes, p.stream);
+    });
+}
+
+int rs_reconstruct_stripes_parts(rs_ctx* c, const rs_stripe_part* parts, size_t pitch, size_t len,
+                                 const uint8_t* erased) {
+    if (!c || !parts || !erased) return RS_EINVAL;
+    const int cnt = members_of(c);
+    std::vector<size_t> first(static_cast<size_t>(cnt) + 1, 0);  // part i's stripes start at first[i]
+    for (int i = 0; i < cnt; ++i) first[i + 1] = first[i] + parts[i].stripes;
+    return run_members(c, [&](int i) -> int {
+        const rs_stripe_part& p = parts[i];
+        if (!p.stripes) return RS_OK;
+        return rs_reconstruct_stripes(member_of(c, i), p.data, p.data_stripe_stride, p.parity, p.parity_stripe_stride,
+                                      pitch, len, p.stripes, erased + first[i] * static_cast<size_t>(c->n), p.stream);
+    });
+}
+
+int rs_reconstruct_spread(rs_ctx* c, const uint64_t* shard_ptrs, const int* owner, size_t len, size_t stripes,
+                          const uint8_t* erased, void* const* streams) {
+    if (!c || !shard_ptrs || !owner || !erased) return RS_EINVAL;
+    if (stripes == 0 || len == 0) return RS_OK;
+    if (round_up(len, 16) / 16 >= (size_t(1) << 28)) return RS_EINVAL;  // 32-bit column offsets
+    const int cnt = members_of(c);
+    for (size_t s = 0; s < stripes; ++s)
+        if (owner[s] < 0 || owner[s] >= cnt) return RS_EINVAL;
+    if (c->set && !rsmi::set_peer_ok(c->set)) return RS_EDEVICE;  // survivors on a GPU the owner cannot read
+    const size_t n = static_cast<size_t>(c->n);
+    return run_members(c, [&](int i) -> int {
+        // Member i's stripes, in stripe order: their rows of the address
+        // table and of the erasure flags.
+        std::vector<uint64_t> tab;
+        std::vector<uint8_t> er;
+        for (size_t s = 0; s < stripes; ++s) {
+            if (owner[s] != i) continue;
+            tab.insert(tab.end(), shard_ptrs + s * n, shard_ptrs + (s + 1) * n);
+            er.insert(er.end(), erased + s * n, erased + (s + 1) * n);
+        }
+        if (tab.empty()) return RS_OK;
+        const hipStream_t st = streams ? static_cast<hipStream_t>(streams[i]) : nullptr;
+        return reconstruct_host_table(member_of(c, i), tab.data(), len, tab.size() / n, er.data(), st);
+    });
 }
 
 int rs_fill_splitmix(rs_ctx* c, void* dev, size_t len, uint64_t seed, void* stream) {
     if (!c || (!dev && len)) return RS_EINVAL;
     if (reinterpret_cast<uintptr_t>(dev) & 7u) return RS_EINVAL;
+    if (c->set) {
+        rs_ctx* mc = routed(c, dev);
+        return mc ? rs_fill_splitmix(mc, dev, len, seed, stream) : RS_EINVAL;
+    }
     DeviceGuard g(c->device);
     if (!g.ok) return RS_EDEVICE;
     return hip_status(rsmi::launch_fill_splitmix(dev, len, seed, static_cast<hipStream_t>(stream)));

@@ -22,8 +22,11 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"os"
 	"runtime"
 	"sort"
+	"strconv"
+	"strings"
 	"sync"
 	"unsafe"
 )
@@ -61,15 +64,17 @@ func statusErr(st C.int) error {
 	}
 }
 
-// FEC is a (k, n) code bound to one GPU context.  The context is shared by
-// every FEC with the same (k, n) in the process (the plugin calls NewFEC for
-// every message, main.go:73/:248; building and uploading tables each time
-// would dominate small messages).
+// FEC is a (k, n) code bound to one GPU context -- or to a device-set
+// context over several GPUs (NewFECOnDevices, or NewFEC with RSMI_DEVICES
+// set).  NewFEC's context is shared by every FEC with the same (k, n) in the
+// process (the plugin calls NewFEC for every message, main.go:73/:248;
+// building and uploading tables each time would dominate small messages).
 type FEC struct {
-	k, n int
-	ctx  *C.rs_ctx
-	mu   sync.Mutex // guards parity (reused between Encode calls like infectious)
-	par  []byte
+	k, n  int
+	ctx   *C.rs_ctx
+	owned bool       // made by NewFECOnDevices: Close frees it
+	mu    sync.Mutex // guards parity (reused between Encode calls like infectious)
+	par   []byte
 }
 
 var (
@@ -77,21 +82,102 @@ var (
 	ctxCache = map[[2]int]*C.rs_ctx{}
 )
 
-// NewFEC mirrors infectious.NewFEC(k, n): error unless 1 <= k <= n <= 256.
-func NewFEC(k, n int) (*FEC, error) {
+func checkKN(k, n int) error {
 	if k <= 0 || n <= 0 || k > 256 || n > 256 || k > n {
-		return nil, errors.New("requires 1 <= k <= n <= 256")
+		return errors.New("requires 1 <= k <= n <= 256")
+	}
+	return nil
+}
+
+// envDevices parses RSMI_DEVICES ("0,1,2,3,4,5,6,7"): the GPUs NewFEC's
+// shared contexts span, so the unchanged plugin (main.go changes only its
+// import) partitions its work over every GPU of the node.  Empty: one GPU.
+func envDevices() ([]int, error) {
+	v := strings.TrimSpace(os.Getenv("RSMI_DEVICES"))
+	if v == "" {
+		return nil, nil
+	}
+	var devs []int
+	for _, f := range strings.Split(v, ",") {
+		d, err := strconv.Atoi(strings.TrimSpace(f))
+		if err != nil || d < 0 {
+			return nil, fmt.Errorf("infectious: bad RSMI_DEVICES entry %q", f)
+		}
+		devs = append(devs, d)
+	}
+	return devs, nil
+}
+
+func newDeviceSet(k, n int, devices []int) (*C.rs_ctx, error) {
+	cnt := len(devices)
+	devs := (*[1 << 16]C.int)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(C.int(0)))))[:cnt:cnt]
+	defer C.free(unsafe.Pointer(&devs[0]))
+	for i, d := range devices {
+		devs[i] = C.int(d)
+	}
+	var ctx *C.rs_ctx
+	if st := C.rs_new_devices(C.int(k), C.int(n), &devs[0], C.int(cnt), &ctx); st != C.RS_OK {
+		return nil, statusErr(st)
+	}
+	return ctx, nil
+}
+
+// NewFEC mirrors infectious.NewFEC(k, n): error unless 1 <= k <= n <= 256.
+// With RSMI_DEVICES set the shared context is a device set over those GPUs.
+func NewFEC(k, n int) (*FEC, error) {
+	if err := checkKN(k, n); err != nil {
+		return nil, err
 	}
 	ctxMu.Lock()
 	defer ctxMu.Unlock()
 	ctx, ok := ctxCache[[2]int{k, n}]
 	if !ok {
-		if st := C.rs_new(C.int(k), C.int(n), &ctx); st != C.RS_OK {
+		devs, err := envDevices()
+		if err != nil {
+			return nil, err
+		}
+		if len(devs) > 0 {
+			if ctx, err = newDeviceSet(k, n, devs); err != nil {
+				return nil, err
+			}
+		} else if st := C.rs_new(C.int(k), C.int(n), &ctx); st != C.RS_OK {
 			return nil, statusErr(st)
 		}
 		ctxCache[[2]int{k, n}] = ctx
 	}
 	return &FEC{k: k, n: n, ctx: ctx}, nil
+}
+
+// NewFECOnDevices is NewFEC over several GPUs (not in infectious): one
+// device-set context (rs_new_devices) with a member per listed HIP device
+// (north_star: stripes partitioned over the GPUs of one node).  Encode and
+// Decode run on the least busy GPU; EncodeBatch and DecodeBatch split their
+// messages into contiguous ranges, one per GPU, all at once.  The context is
+// the caller's (not cached): Close frees it.
+func NewFECOnDevices(k, n int, devices []int) (*FEC, error) {
+	if err := checkKN(k, n); err != nil {
+		return nil, err
+	}
+	if len(devices) == 0 {
+		return nil, errors.New("infectious: no devices")
+	}
+	ctx, err := newDeviceSet(k, n, devices)
+	if err != nil {
+		return nil, err
+	}
+	return &FEC{k: k, n: n, ctx: ctx, owned: true}, nil
+}
+
+// Devices is the number of GPUs the FEC's context spans.
+func (f *FEC) Devices() int { return int(C.rs_member_count(f.ctx)) }
+
+// Close frees a context made by NewFECOnDevices; NewFEC's shared contexts
+// live for the process.
+func (f *FEC) Close() {
+	if f.owned && f.ctx != nil {
+		C.rs_free(f.ctx)
+		f.ctx = nil
+	}
 }
 
 // Required is the number of shares needed to reconstruct (k).

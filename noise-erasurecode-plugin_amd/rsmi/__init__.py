@@ -44,7 +44,17 @@ EXPORTS = (
     "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
     "rs_blake2b_batch", "rs_blake2b_device", "rs_blake2b", "rs_blake2b_host",
     "rs_stat", "rs_arena_new", "rs_arena_alloc", "rs_arena_reset", "rs_arena_used", "rs_arena_free",
+    "rs_new_devices", "rs_member_count", "rs_member", "rs_partition",
+    "rs_encode_stripes_parts", "rs_reconstruct_stripes_parts", "rs_reconstruct_spread",
 )
+
+
+class StripePart(ctypes.Structure):
+    """rs_stripe_part (include/rsmi.h): the stripes one member holds."""
+
+    _fields_ = [("data", ctypes.c_void_p), ("data_stripe_stride", ctypes.c_size_t),
+                ("parity", ctypes.c_void_p), ("parity_stripe_stride", ctypes.c_size_t),
+                ("stripes", ctypes.c_size_t), ("stream", ctypes.c_void_p)]
 
 
 class RSError(Exception):
@@ -112,6 +122,13 @@ def _lib() -> ctypes.CDLL:
             "rs_blake2b_device": (i32, [vp, i32, vp, vp, vp, i32, vp, vp]),
             "rs_blake2b": (i32, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp, ctypes.POINTER(i32)]),
             "rs_blake2b_host": (i32, [i32, ctypes.POINTER(vp), ctypes.POINTER(sz), i32, vp, i32]),
+            "rs_new_devices": (i32, [i32, i32, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]),
+            "rs_member_count": (i32, [vp]),
+            "rs_member": (vp, [vp, i32]),
+            "rs_partition": (i32, [sz, i32, i32, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+            "rs_encode_stripes_parts": (i32, [vp, ctypes.POINTER(StripePart), sz, sz]),
+            "rs_reconstruct_stripes_parts": (i32, [vp, ctypes.POINTER(StripePart), sz, sz, vp]),
+            "rs_reconstruct_spread": (i32, [vp, vp, vp, sz, sz, vp, vp]),
         }
         for name, (res, args) in sig.items():
             if os.environ.get("RSMI_LIB") and not hasattr(lib, name):
@@ -147,20 +164,82 @@ class Share:
         return Share(self.Number, bytes(self.Data))
 
 
-class FEC:
-    """Handle of an rs_ctx: the engine-side infectious *FEC for (k, n)."""
+def partition(units: int, parts: int, part: int):
+    """rs_partition: (first, count) of part `part` of `units` split into
+    `parts` contiguous ranges."""
+    first, count = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(_lib().rs_partition(units, parts, part, ctypes.byref(first), ctypes.byref(count)), "rs_partition")
+    return first.value, count.value
 
-    def __init__(self, k: int, n: int, device: Optional[int] = None):
+
+class FEC:
+    """Handle of an rs_ctx: the engine-side infectious *FEC for (k, n).
+    devices=[...] builds a device-set context (rs_new_devices): one member
+    per listed GPU, every call spread over them."""
+
+    def __init__(self, k: int, n: int, device: Optional[int] = None,
+                 devices: Optional[Sequence[int]] = None, _handle=None):
         lib = _lib()
+        self.k = k
+        self.n = n
+        self._owner = _handle is None
+        if _handle is not None:  # a member of a device set: owned by the set
+            self._h = ctypes.c_void_p(_handle)
+            return
         h = ctypes.c_void_p()
-        if device is None:
+        if devices is not None:
+            devs = (ctypes.c_int * max(len(devices), 1))(*devices)
+            code = lib.rs_new_devices(k, n, devs, len(devices), ctypes.byref(h))
+        elif device is None:
             code = lib.rs_new(k, n, ctypes.byref(h))
         else:
             code = lib.rs_new_on_device(k, n, device, ctypes.byref(h))
         _check(code, f"NewFEC({k}, {n})")
         self._h = h
-        self.k = k
-        self.n = n
+
+    # -- device sets (rs_new_devices) --------------------------------------------
+    def member_count(self) -> int:
+        return _lib().rs_member_count(self._h)
+
+    def member(self, i: int) -> "FEC":
+        """Member i (a single-device context owned by the set; self for i = 0
+        of a single-device context)."""
+        h = _lib().rs_member(self._h, i)
+        if not h:
+            raise RSError(RS_EINVAL, f"rs_member({i})")
+        m = FEC(self.k, self.n, _handle=h)
+        m._set = self  # keep the set alive while the member is used
+        return m
+
+    def encode_stripes_parts(self, parts: Sequence[tuple], pitch: int, shard_len: int) -> None:
+        """rs_encode_stripes_parts: parts[i] = (data_ptr, data_stride,
+        parity_ptr, parity_stride, stripes, stream) on member i's device."""
+        arr = (StripePart * max(len(parts), 1))(*[StripePart(*p) for p in parts])
+        _check(_lib().rs_encode_stripes_parts(self._h, arr, pitch, shard_len), "rs_encode_stripes_parts")
+
+    def reconstruct_stripes_parts(self, parts: Sequence[tuple], pitch: int, shard_len: int,
+                                  erased: bytes) -> None:
+        arr = (StripePart * max(len(parts), 1))(*[StripePart(*p) for p in parts])
+        buf = ctypes.c_char_p(bytes(erased))
+        _check(_lib().rs_reconstruct_stripes_parts(self._h, arr, pitch, shard_len,
+                                                   ctypes.cast(buf, ctypes.c_void_p)),
+               "rs_reconstruct_stripes_parts")
+
+    def reconstruct_spread(self, shard_ptrs: Sequence[int], owner: Sequence[int], shard_len: int,
+                           stripes: int, erased: bytes, streams: Optional[Sequence[int]] = None) -> None:
+        """rs_reconstruct_spread: shard i of stripe s at device address
+        shard_ptrs[s * n + i] on any member's GPU; owner[s] reconstructs."""
+        import numpy as np
+        if len(erased) != stripes * self.n or len(shard_ptrs) != stripes * self.n or len(owner) != stripes:
+            raise RSError(RS_EINVAL, "reconstruct_spread: table sizes")
+        tab = np.ascontiguousarray(np.asarray(shard_ptrs, dtype=np.uint64))
+        own = np.ascontiguousarray(np.asarray(owner, dtype=np.int32))
+        buf = ctypes.c_char_p(bytes(erased))
+        st = None
+        if streams is not None:
+            st = (ctypes.c_void_p * max(len(streams), 1))(*[x or None for x in streams])
+        _check(_lib().rs_reconstruct_spread(self._h, tab.ctypes.data, own.ctypes.data, shard_len, stripes,
+                                            ctypes.cast(buf, ctypes.c_void_p), st), "rs_reconstruct_spread")
 
     # -- infectious accessors -------------------------------------------------
     def Required(self) -> int:
@@ -175,7 +254,8 @@ class FEC:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            _lib().rs_free(self._h)
+            if getattr(self, "_owner", True):
+                _lib().rs_free(self._h)
             self._h = None
 
     def __del__(self):

@@ -9,7 +9,9 @@
  * rs_decode with shares in arrival order (sorted in place); receive-side
  * batching -> rs_decode_batch with ShardData unmarshalled into an rs_arena
  * (zero-copy); send-side batching -> rs_encode_batch; the blake2b hash policy -> rs_blake2b_batch (RFC 7693 known
- * answers); error classes; 8 pthreads decoding on one context.
+ * answers); error classes; 8 pthreads decoding on one context; the same
+ * host calls on a device-set context (rs_new_devices over {0, 0}: two members
+ * on the box's one GPU), the way the shim's NewFECOnDevices drives it.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -83,7 +85,8 @@ static void check_encode_batch(rs_ctx *ctx, int k, int n, size_t len, int B) {
     }
     const int64_t batches0 = rs_stat(ctx, RS_STAT_ENCODE_BATCHES);
     CHECK(rs_encode_batch(ctx, B, ins, len, outs, st) == RS_OK, "rs_encode_batch");
-    CHECK(rs_stat(ctx, RS_STAT_ENCODE_BATCHES) == batches0 + 1, "rs_encode_batch not batched");
+    /* one batched pass per member (a device set splits the messages) */
+    CHECK(rs_stat(ctx, RS_STAT_ENCODE_BATCHES) == batches0 + rs_member_count(ctx), "rs_encode_batch not batched");
     uint8_t *ref = malloc(m * S);
     for (int b = 0; b < B; b++) {
         CHECK(orc_encode(enc, k, n, ins[b], len, ref) == 0, "orc_encode");
@@ -135,7 +138,7 @@ static void check_arena_batch(rs_ctx *ctx, int k, int n, size_t S, int B) {
     CHECK(rs_decode_batch(ctx, B, counts, nums, ptrs, S, dsts, st) == RS_OK, "rs_decode_batch");
     for (int b = 0; b < B; b++)
         CHECK(st[b] == RS_OK && memcmp(dsts[b], inputs[b], (size_t)k * S) == 0, "batch message %d", b);
-    CHECK(rs_stat(ctx, RS_STAT_BATCHES_IN_PLACE) == in_place0 + 1, "batch not read in place");
+    CHECK(rs_stat(ctx, RS_STAT_BATCHES_IN_PLACE) == in_place0 + rs_member_count(ctx), "batch not read in place");
     for (int b = 0; b < B; b++) { free(inputs[b]); free(dsts[b]); }
     free(inputs); free(dsts); free(counts); free(nums); free(st); free(ptrs);
     rs_arena_free(arena);
@@ -235,6 +238,34 @@ int main(void) {
     }
     printf("abi_check: %lld leases on the RS(10,4) context after 8 concurrent decoders\n",
            (long long)rs_stat(c10, RS_STAT_LEASES));
+    /* Device set {0, 0}: the plugin process's multi-GPU context (north_star's
+     * stripe partition behind the C ABI), two members on one GPU here. */
+    {
+        const int devs[2] = {0, 0};
+        rs_ctx *set = NULL;
+        CHECK(rs_new_devices(10, 14, devs, 2, &set) == RS_OK && set, "rs_new_devices");
+        if (set) {
+            CHECK(rs_member_count(set) == 2 && rs_member(set, 1) && !rs_member(set, 2), "members");
+            size_t f0 = 0, n0 = 0, f1 = 0, n1 = 0;
+            CHECK(rs_partition(24, 2, 0, &f0, &n0) == RS_OK && rs_partition(24, 2, 1, &f1, &n1) == RS_OK &&
+                      f0 == 0 && n0 == 12 && f1 == 12 && n1 == 12, "rs_partition");
+            check_encode_decode(set, 10, 14, 1048580, 0x5E7);
+            check_encode_batch(set, 10, 14, 1048580, 24); /* 12 + 12 messages, one pass per member */
+            check_arena_batch(set, 10, 14, 6554, 64);
+            check_blake2b(set);
+            for (int t = 0; t < 8; t++) {
+                jobs[t] = (struct job){set, 100 + t, 0};
+                pthread_create(&th[t], NULL, decode_worker, &jobs[t]);
+            }
+            for (int t = 0; t < 8; t++) {
+                pthread_join(th[t], NULL);
+                CHECK(jobs[t].ok, "device-set concurrent decode thread %d", t);
+            }
+            CHECK(rs_stat(rs_member(set, 0), RS_STAT_LEASES) >= 1 && rs_stat(rs_member(set, 1), RS_STAT_LEASES) >= 1,
+                  "both members served calls");
+            rs_free(set);
+        }
+    }
     rs_free(c10);
     rs_free(c64);
     rs_free(c4);

@@ -108,3 +108,14 @@ def test_go_shim_keeps_infectious_api_names():
                 r"type Share struct", r"func \(s \*?Share\) DeepCopy\(\)",
                 r"func \(f \*FEC\) Required\(\) int", r"func \(f \*FEC\) Total\(\) int"):
         assert re.search(pat, src), pat
+
+
+def test_go_shim_exposes_device_sets():
+    """NewFECOnDevices: the plugin process spans several
+    GPUs through one device-set context; NewFEC honours RSMI_DEVICES so the
+    unchanged plugin can too."""
+    src = open(GO).read()
+    assert re.search(r"func NewFECOnDevices\(k, n int, devices \[\]int\) \(\*FEC, error\)", src)
+    assert "C.rs_new_devices(" in src and "RSMI_DEVICES" in src
+    assert re.search(r"func \(f \*FEC\) Close\(\)", src)
+

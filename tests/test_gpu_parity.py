@@ -1006,23 +1006,37 @@ def test_host_api_pinned_buffers(k, n, S):
             lib.rs_pinned_free(p)
 
 
+# Where each kept share sits relative to dst (rows of S bytes; dst row r is
+# buffer row r + 1, so row -1 is just before dst).  Lost: data shares 0-3.
+_ALIAS_LAYOUTS = {
+    # share i one row after its own: copying share i to row i overwrites i - 1
+    "plus1": lambda keep, k: {i: i + 1 for i in keep},
+    # one row before its own: share i is overwritten by share i + 1's copy
+    # before it is read
+    "minus1": lambda keep, k: {i: i - 1 for i in keep},
+    # Rebuild's parity survivors stored in the missing data rows the kernel
+    # writes; present data shares in their own rows
+    "missing_rows": lambda keep, k: {i: (i if i < k else i - k) for i in keep},
+    # every share in dst, in reverse order
+    "reversed": lambda keep, k: {i: k - 1 - j for j, i in enumerate(keep)},
+}
+
+
+@pytest.mark.parametrize("layout", sorted(_ALIAS_LAYOUTS))
 @pytest.mark.parametrize("pinned", [True, False])
 @pytest.mark.parametrize("S", [4096, 104858, 300000])
-def test_decode_dst_overlapping_survivors(pinned, S):
-    """rs_decode copies the present data shares into dst while
-    the GPU reads the survivors -- in place when they are engine-pinned.  Here
-    the shares live INSIDE dst, one row later than their own (share i at row
-    i + 1), so copying share i to row i overwrites share i - 1 where the
-    kernel reads it; the engine must copy only after the kernel.  The decoded
-    bytes equal the original data (engine-pinned and pageable memory; staged,
-    chunked and pipelined sizes)."""
+def test_decode_dst_overlapping_survivors(pinned, S, layout):
+    """infectious lets Decode's shares alias dst.  rs_decode writes dst while
+    the GPU still reads survivors -- in place when they are engine-pinned --
+    and moves present shares within dst; the engine sets aliasing shares aside
+    first.  Every layout decodes to the original data
+    (engine-pinned and pageable memory; staged, chunked and pipelined sizes)."""
     import ctypes
     lib = rsmi.load()
     k, n = 10, 14
-    m = n - k
     f = fec(k, n)
     data, sh = _shards(k, n, S, 4321 + S)
-    size = (n + 1) * S
+    size = (n + 2) * S
     buf = lib.rs_pinned_alloc(size) if pinned else None
     keep_alive = None
     if not pinned:
@@ -1030,16 +1044,15 @@ def test_decode_dst_overlapping_survivors(pinned, S):
         buf = ctypes.addressof(keep_alive)
     assert buf
     try:
-        for i in range(n):
-            ctypes.memmove(buf + (i + 1) * S, sh[i], S)
-        # data shares 0-3 lost: their outputs (rows 0-3) overwrite no survivor;
-        # copying present share i (row i + 1) to row i overwrites share i - 1
         lost = [0, 1, 2, 3]
         keep = [i for i in range(n) if i not in lost]
+        row = _ALIAS_LAYOUTS[layout](keep, k)
+        for i in keep:
+            ctypes.memmove(buf + (row[i] + 1) * S, sh[i], S)
         nums = (ctypes.c_int * k)(*keep)
-        ptrs = (ctypes.c_void_p * k)(*[buf + (i + 1) * S for i in keep])
-        assert lib.rs_decode(f.handle, nums, ptrs, k, S, buf) == rsmi.RS_OK
-        assert ctypes.string_at(buf, k * S) == data
+        ptrs = (ctypes.c_void_p * k)(*[buf + (row[i] + 1) * S for i in keep])
+        assert lib.rs_decode(f.handle, nums, ptrs, k, S, buf + S) == rsmi.RS_OK
+        assert ctypes.string_at(buf + S, k * S) == data
     finally:
         if pinned:
             lib.rs_pinned_free(buf)
