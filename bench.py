@@ -97,6 +97,9 @@ def parse():
     ap.add_argument("--gather-timeout", type=float, default=180.0,
                     help="seconds after which a stuck gather leg is abandoned (the line is still printed, "
                          f"then the ranks exit {EXIT_GATHER_ABANDONED})")
+    ap.add_argument("--device-set-stripes", type=int, default=512,
+                    help="stripes per member of the device-set leg (rank 0: one rs_new_devices context over every "
+                         "visible GPU, [0, 0] on a one-GPU box; never value); 0 skips")
     ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
                     help="N = 1: skip the configs[0] (per-message latency), configs[4] (RS(64,16)) and "
                          "configs[2] worst-case legs reported beside the headline")
@@ -648,6 +651,153 @@ def config5_leg(local, dev, stripes=16384, steps=5, warmup=2):
     }
 
 
+def device_set_leg(k, n, S, stripes, steps=3, warmup=1, spread_stripes=256, seed=0xD5E7):
+    """north_star's node-level partition through the product boundary (VERDICT
+    r05 next #1): ONE process, one device-set context (rs_new_devices, the
+    Go shim's NewFECOnDevices) over every GPU this process sees -- [0, 0], two
+    members on one GPU, on a one-GPU box.  Member i holds its own `stripes`
+    stripes in its own HBM; a step is rs_encode_stripes_parts then
+    rs_reconstruct_stripes_parts with fresh 1..m erasures per stripe, every
+    member at once from its own host thread, timed by the wall clock around
+    every device's synchronize.  Then the shard-distributed placement
+    (configs[3]): shard i of each of `spread_stripes` stripes
+    on GPU i mod G, stripe s reconstructed by member s mod G with
+    rs_reconstruct_spread -- survivors on other GPUs read in place over xGMI
+    (peer access).  Both checked: erased shards zeroed, reconstructed, and
+    every member's buffers equal their checksums from before.  Never `value`."""
+    import rsmi
+    m = n - k
+    G = torch.cuda.device_count()
+    devices = list(range(G)) if G > 1 else [0, 0]
+    f = rsmi.FEC(k, n, devices=devices)
+    M = f.member_count()
+    data = [torch.empty(stripes * k * S, dtype=torch.uint8, device=f"cuda:{d}") for d in devices]
+    par = [torch.empty(stripes * m * S, dtype=torch.uint8, device=f"cuda:{d}") for d in devices]
+
+    def sync():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    for i in range(M):
+        f.member(i).fill_splitmix(data[i].data_ptr(), data[i].numel(), seed + i)
+    parts = [(data[i].data_ptr(), k * S, par[i].data_ptr(), m * S, stripes, 0) for i in range(M)]
+    if pattern_total(n, m) <= (1 << 20):
+        f.prepare_patterns(m)  # every member's cache, before timing (like the headline)
+    f.encode_stripes_parts(parts, S, S)
+    sync()
+
+    def checksum(ts):
+        return [int(t.view(torch.int64).sum().item()) for t in ts]
+
+    ck = (checksum(data), checksum(par))
+    rng = np.random.default_rng(seed)
+    ersets = erasure_sets(rng, warmup + steps + 1, stripes * M, n, 1, m)
+    enc_s, rec_s = [], []
+    for i in range(warmup + steps):
+        t0 = time.perf_counter()
+        f.encode_stripes_parts(parts, S, S)
+        sync()
+        t1 = time.perf_counter()
+        f.reconstruct_stripes_parts(parts, S, S, ersets[i].tobytes())  # intact shards: the same bytes rewritten
+        sync()
+        t2 = time.perf_counter()
+        if i >= warmup:
+            enc_s.append(t1 - t0)
+            rec_s.append(t2 - t1)
+
+    def zero_erased(er, views):
+        for i, (dv, pv) in enumerate(views):
+            e = torch.from_numpy(er[i * stripes:(i + 1) * stripes].astype(bool)).to(dv.device)
+            dv[e[:, :k]] = 0
+            pv[e[:, k:]] = 0
+
+    er = ersets[-1]
+    zero_erased(er, [(data[i].view(stripes, k, S), par[i].view(stripes, m, S)) for i in range(M)])
+    f.reconstruct_stripes_parts(parts, S, S, er.tobytes())
+    sync()
+    ok = (checksum(data), checksum(par)) == ck
+    enc_bytes = M * stripes * n * S
+    rec_bytes = sum(int(((k + x.sum(axis=1)) * S).sum()) for x in ersets[warmup:warmup + steps]) / steps
+    enc_ms, rec_ms = np.median(enc_s) * 1e3, np.median(rec_s) * 1e3
+    out = {
+        "status": "ok" if ok else "error: reconstructed shards differ from the encoded stripes",
+        "what": f"one process, one rs_new_devices context over devices {devices}: RS({k},{n}), "
+                f"{stripes} stripes x {k} x {S} B per member; step = rs_encode_stripes_parts + "
+                f"rs_reconstruct_stripes_parts (fresh 1-{m} erasures), wall clock around every device's "
+                "synchronize; never value",
+        "members": M, "devices": devices, "stripes_per_member": stripes, "steps": steps,
+        "encode": {"ms": round(enc_ms, 3), "GBps": round(enc_bytes / enc_ms / 1e6, 1)},
+        "reconstruct": {"ms": round(rec_ms, 3), "GBps": round(rec_bytes / rec_ms / 1e6, 1)},
+        "value_GBps": round((enc_bytes + rec_bytes) / (enc_ms + rec_ms) / 1e6, 1),
+        "per_gpu_GBps": round((enc_bytes + rec_bytes) / (enc_ms + rec_ms) / 1e6 / len(set(devices)), 1),
+        "checked": ok,
+    }
+    del data, par
+    torch.cuda.empty_cache()
+    # Shard-distributed placement: holders on GPU h = i mod H (H = G, or two
+    # allocations on one GPU), owner of stripe s = member s mod M.
+    try:
+        H = G if G > 1 else 2
+        hdev = list(range(G)) if G > 1 else [0, 0]
+        T = spread_stripes
+        per = [len(range(h, n, H)) for h in range(H)]
+        src_d = torch.empty(T * k * S, dtype=torch.uint8, device=f"cuda:{devices[0]}")
+        src_p = torch.empty(T * m * S, dtype=torch.uint8, device=f"cuda:{devices[0]}")
+        f.member(0).fill_splitmix(src_d.data_ptr(), src_d.numel(), seed ^ 0x5D)
+        f.member(0).encode_stripes(src_d.data_ptr(), k * S, src_p.data_ptr(), m * S, S, S, T)
+        sync()
+        full = torch.cat([src_d.view(T, k, S), src_p.view(T, m, S)], dim=1)
+        holders = [torch.empty(T * per[h] * S, dtype=torch.uint8, device=f"cuda:{hdev[h]}") for h in range(H)]
+        for h in range(H):
+            holders[h].view(T, per[h], S).copy_(full[:, h::H, :])
+        del full, src_d, src_p
+        sync()
+        ptrs = np.zeros((T, n), dtype=np.uint64)
+        for s_ in range(T):
+            for i in range(n):
+                h = i % H
+                ptrs[s_, i] = holders[h].data_ptr() + (s_ * per[h] + i // H) * S
+        owner = [s_ % M for s_ in range(T)]
+        hck = checksum(holders)
+        sets = erasure_sets(np.random.default_rng(seed + 1), warmup + steps + 1, T, n, 1, m)
+        tab = ptrs.reshape(-1).tolist()
+        sp_s = []
+        for i in range(warmup + steps):
+            t0 = time.perf_counter()
+            f.reconstruct_spread(tab, owner, S, T, sets[i].tobytes())
+            sync()
+            if i >= warmup:
+                sp_s.append(time.perf_counter() - t0)
+        er = sets[-1]
+        for s_ in range(T):
+            for i in np.flatnonzero(er[s_]):
+                h = int(i) % H
+                holders[h].view(T, per[h], S)[s_, int(i) // H].zero_()
+        f.reconstruct_spread(tab, owner, S, T, er.tobytes())
+        sync()
+        sok = checksum(holders) == hck
+        # survivor / output bytes that live on another GPU than the owner's
+        remote = 0
+        for s_ in range(T):
+            od = devices[owner[s_]]
+            for i in range(n):
+                remote += (hdev[i % H] != od) and G > 1
+        sp_ms = np.median(sp_s) * 1e3
+        sp_bytes = sum(int(((k + x.sum(axis=1)) * S).sum()) for x in sets[warmup:warmup + steps]) / steps
+        out["spread"] = {
+            "status": "ok" if sok else "error: spread reconstruct differs",
+            "stripes": T, "holders": hdev, "ms": round(sp_ms, 3), "GBps": round(sp_bytes / sp_ms / 1e6, 1),
+            "remote_shard_fraction": round(remote / (T * n), 3),
+            "what": "shard i of every stripe on GPU i mod G, stripe s reconstructed by member s mod G reading "
+                    "its survivors in place (peer HBM over xGMI when G > 1)"}
+        del holders
+        torch.cuda.empty_cache()
+    except Exception as e:  # reported in the leg, never silent
+        out["spread"] = {"status": f"error: {type(e).__name__}: {e}"}
+    f.close()
+    return out
+
+
 def main():
     global _RESULT_OUT
     args = parse()
@@ -796,6 +946,16 @@ def main():
                           "encode_ms": round(v[1], 3), "reconstruct_ms": round(v[2], 3)}
                          for r, v in enumerate(per_rank)],
         }
+    if args.device_set_stripes > 0 and (world > 1 or args.extra_legs):
+        # The device-set context over every GPU this process sees, run by rank
+        # 0 alone while the other ranks wait (after the headline is measured).
+        del f
+        torch.cuda.empty_cache()
+        if rank == 0:
+            out["device_set"] = guarded_leg(lambda: device_set_leg(k, n, S, args.device_set_stripes))
+        if distributed:
+            torch.distributed.barrier()
+        f = rsmi.FEC(k, n, device=local)
     if distributed and world > 1 and args.gather_stripes > 0:
         # configs[3]'s survivor gather on the same ranks, after the headline
         # is measured (device_run freed its buffers).

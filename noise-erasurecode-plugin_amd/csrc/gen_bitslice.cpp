@@ -89,14 +89,44 @@ bool kBufferLoads = true;
 // the RS(64,16) kernel's ISA, same-box A/B 10 steps x 2 (profiles/r04h/):
 // config 5 fresh -0.4..-0.9%, pool -0.4..-0.8%, 16 erasures -0.1%.
 bool kInputBarrier = false;
-// Solve tail (-L): outputs past e in the last group of R are skipped by a
-// wave-uniform branch per (syndrome, output) instead of coded as padding;
-// the syndrome's bit fields are extracted once per group for all outputs.
-bool kSolveTail = false;
+// Solve tail (default; -l: off): outputs past e in the last group of R are
+// skipped by a wave-uniform branch per (syndrome, output) instead of coded as
+// padding (for e uniform in 1..16, 1.5 of every 10 outputs coded were
+// padding); the syndrome's bit fields are extracted once per group for all
+// outputs.  With -W, same-box A/B against neither, config 5, 5 steps x 2
+// (profiles/r06c/): fresh 1-16 -1.2%, pool of 256 -1.5%, e = 16 -1.0%.
+bool kSolveTail = true;
+// Solve in bit planes (-S; measured slower, so off: the split-table solve):
+// the syndromes stay in planes, and an output gets c * s as the XOR of the
+// planes of 2^b * s over the set bits b of c -- 2^b * s is s advanced b times
+// by the fixed map x -> 2x (a plane rotation plus 3 XORs, shared by every
+// output), the bits of c are wave-uniform scalar branches.  Per (output,
+// syndrome) pair and 32 bytes: ~4 x 8 XORs + 21 / R shared, where the split
+// tables issue 24 v_perm (slow class) + 16 XOR + the syndrome's bit fields;
+// each parity survivor is transposed into planes instead of its row out of
+// them, and each output leaves the planes at its store.  Same-box A/B,
+// config 5, 5 steps x 2 (profiles/r06b/): e = 16 23.3 vs 22.1 ms, fresh
+// 1-16 17.4 vs 16.8, pool of 256 15.4 vs 14.7 -- fewer VALU, but the 512
+// wave-uniform branches per output group (s_bitcmp + s_cbranch per bit) cost
+// more than the v_perm tables they replace.
+bool kPlaneSolve = false;
+// Transpose stages 4 and 2 with one 64-bit left shift per pair of words
+// (-W): v_lshlrev_b64 issues at the rate of one v_lshlrev_b32 (profiles/
+// r02bm/shift64.log), so each stage needs 2 slow shifts instead of 4; the
+// bits a 64-bit shift carries across the word boundary land where the select
+// mask keeps the other operand.  On by default (-w: off; A/B in kSolveTail's
+// note); the bit-sliced encode is at its movement ceiling either way (13.97-
+// 14.18 vs 14.06 ms, profiles/r06c/enc.log).
+bool kShift64 = true;
 constexpr int kTopMinM = 12;
 
 void emit_common(FILE* f) {
-    std::fputs(R"(// GENERATED by gen_bitslice.cpp -- do not edit (rebuilt by the Makefile).
+    std::fputs("// GENERATED by gen_bitslice.cpp -- do not edit (rebuilt by the Makefile).\n", f);
+    std::fprintf(f, "// The reconstruct's solve: in bit planes (1; gen_bitslice -S) or split tables (0).\n"
+                    "#define BS_PLANE_SOLVE %d\n"
+                    "// Transpose stages 4 and 2 with 64-bit left shifts (gen_bitslice -W).\n"
+                    "#define BS_SHIFT64 %d\n", kPlaneSolve && !kMovementOnly ? 1 : 0, kShift64 ? 1 : 0);
+    std::fputs(R"(
 #include "bitslice.hpp"
 #include "gf_device.hpp"
 #include "xcd.hpp"
@@ -134,16 +164,40 @@ __device__ __forceinline__ void bs_swap(uint32_t& a, uint32_t& b) {
     b = nb;
 }
 
+// Two swaps whose b words are consecutive: one 64-bit left shift for both
+// (BS_SHIFT64).  The S bits b0 carries into the low end of b1's shifted word
+// sit where M selects a1, so they never reach the result.
+template <int S, uint32_t M>
+__device__ __forceinline__ void bs_swap2(uint32_t& a0, uint32_t& a1, uint32_t& b0, uint32_t& b1) {
+    // (inline asm: left to itself hipcc splits the 64-bit shift back into
+    // 32-bit shifts and ors)
+    uint64_t bb;
+    asm("v_lshlrev_b64 %0, %2, %1" : "=v"(bb) : "v"(static_cast<uint64_t>(b1) << 32 | b0), "i"(S));
+    const uint32_t na0 = __builtin_amdgcn_bitop3_b32(M, a0, static_cast<uint32_t>(bb), 0xCA);
+    const uint32_t na1 = __builtin_amdgcn_bitop3_b32(M, a1, static_cast<uint32_t>(bb >> 32), 0xCA);
+    const uint32_t nb0 = __builtin_amdgcn_bitop3_b32(M, a0 >> S, b0, 0xCA);
+    const uint32_t nb1 = __builtin_amdgcn_bitop3_b32(M, a1 >> S, b1, 0xCA);
+    a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
+}
+
 // 8 words of 4 bytes <-> 8 bit planes: word index and in-byte bit index
 // exchange their three bits, one delta-swap stage per bit.  Plane p ends up
 // holding bit p of byte (w, b) at bit position 8b + w.
 __device__ __forceinline__ void bs_stage4(uint32_t (&w)[8]) {
+#if BS_SHIFT64
+    bs_swap2<4, 0x0F0F0F0Fu>(w[0], w[1], w[4], w[5]); bs_swap2<4, 0x0F0F0F0Fu>(w[2], w[3], w[6], w[7]);
+#else
     bs_swap<4, 0x0F0F0F0Fu>(w[0], w[4]); bs_swap<4, 0x0F0F0F0Fu>(w[1], w[5]);
     bs_swap<4, 0x0F0F0F0Fu>(w[2], w[6]); bs_swap<4, 0x0F0F0F0Fu>(w[3], w[7]);
+#endif
 }
 __device__ __forceinline__ void bs_stage2(uint32_t (&w)[8]) {
+#if BS_SHIFT64
+    bs_swap2<2, 0x33333333u>(w[0], w[1], w[2], w[3]); bs_swap2<2, 0x33333333u>(w[4], w[5], w[6], w[7]);
+#else
     bs_swap<2, 0x33333333u>(w[0], w[2]); bs_swap<2, 0x33333333u>(w[1], w[3]);
     bs_swap<2, 0x33333333u>(w[4], w[6]); bs_swap<2, 0x33333333u>(w[5], w[7]);
+#endif
 }
 __device__ __forceinline__ void bs_stage1(uint32_t (&w)[8]) {
     bs_swap<1, 0x55555555u>(w[0], w[1]); bs_swap<1, 0x55555555u>(w[2], w[3]);
@@ -157,6 +211,15 @@ __device__ __forceinline__ void bs_pin8(uint32_t (&w)[8]) {
 }
 __device__ __forceinline__ void bs_to_planes(uint32_t (&w)[8]) { bs_stage4(w); bs_stage2(w); bs_stage1(w); bs_pin8(w); }
 __device__ __forceinline__ void bs_from_planes(uint32_t (&w)[8]) { bs_stage1(w); bs_stage2(w); bs_stage4(w); }
+
+// x -> 2x (GF(2^8), poly 0x11D) on 8 bit planes: bit q of 2x is bit q - 1
+// of x, and bit 7 of x folds back as 0x1D (bits 0, 2, 3, 4).
+__device__ __forceinline__ __attribute__((unused)) void bs_mul2(uint32_t (&y)[8]) {
+    const uint32_t h = y[7];
+    y[7] = y[6]; y[6] = y[5]; y[5] = y[4];
+    y[4] = y[3] ^ h; y[3] = y[2] ^ h; y[2] = y[1] ^ h;
+    y[1] = y[0]; y[0] = h;
+}
 
 // The 16 XOR combinations of 4 planes (c[0] unused).
 __device__ __forceinline__ void bs_combos(const uint32_t* p, uint32_t (&c)[16]) {
@@ -378,10 +441,17 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
     // a separate instantiation, so the strided kernel carries no trace of it.
     std::fprintf(f, "template <bool kPtrs>\n__global__ __launch_bounds__(256) void %s(BitsliceRecArgs a) {\n", name.c_str());
     std::fprintf(f, "    constexpr int K = %d, M = %d, R = %d, NG = %d, TOP = %d, T0 = %d;\n", k, m, kRows, NG, top, T0);
-    std::fprintf(f, "%s", R"(    // Split tables of the syndrome coefficients: mtab[o][t - T0] multiplies
+    std::fprintf(f, "%s", R"(#if BS_PLANE_SOLVE
+    // The syndrome coefficients: byte o of row t - T0 multiplies syndrome t
+    // into output o (zero past the outputs and for parity rows that are not
+    // survivors); one word holds a solve group's R = 4 outputs.
+    __shared__ uint32_t mcoef[TOP][(NG * R + 3) / 4];
+#else
+    // Split tables of the syndrome coefficients: mtab[o][t - T0] multiplies
     // syndrome t into output o (zero past the outputs and for parity rows
     // that are not survivors).
     __shared__ uint32_t mtab[NG * R][TOP][5];
+#endif
     // A stripe's blocks run on one XCD, in order (xcd.hpp).
     const uint32_t bx = a.xcd ? xcd_block(blockIdx.x, a.xcd * a.blocks_per_stripe, gridDim.x) : blockIdx.x;
     const uint64_t sv = bx / a.blocks_per_stripe;
@@ -545,6 +615,14 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
                             "        bs_combos(&%s[4], c2);\n", xb.c_str(), xb.c_str());
             emit_network(f, E, k, m, j, false, top < m && !kTopGuard ? nullptr : "rmask", T0);
             emit_acc_fence(f, 0, P);
+        } else if (kPlaneSolve) {
+            // Parity survivor t: row t's network sum is complete (data inputs
+            // come first); the survivor's planes are XORed in, and acc row t
+            // holds syndrome t in planes for the plane solve.
+            const int t = j - k;  // accumulator row (parity row T0 + t)
+            std::fprintf(f, "        bs_to_planes(%s);\n", xb.c_str());
+            for (int q = 0; q < 8; ++q) std::fprintf(f, "        acc[%d] ^= %s[%d];\n", t * 8 + q, xb.c_str(), q);
+            emit_acc_fence(f, t * 8, t * 8 + 8);
         } else {
             // Parity survivor t: row t's network sum is complete (data inputs
             // come first), so the row goes back to bytes here and the
@@ -566,7 +644,11 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
         for (int q = 0; q < CPT; ++q) {
             const uint32_t idx = threadIdx.x + 256u * q;
             const uint32_t o = idx / TOP, t = idx - o * TOP;
+#if BS_PLANE_SOLVE
+            if (idx < static_cast<uint32_t>(NG * R * TOP)) reinterpret_cast<uint8_t*>(&mcoef[t][0])[o] = static_cast<uint8_t>(tcoef[q]);
+#else
             if (idx < static_cast<uint32_t>(NG * R * TOP)) gfd::build_tables(tcoef[q], &mtab[o][t][0]);
+#endif
         }
     }
 )");
@@ -591,6 +673,74 @@ void emit_reconstruct(FILE* f, int k, int n, int top) {
         uint8_t* o = shard(oid);
         if (oka) bs_store(o, offa, w[0], w[1], w[2], w[3]);
         if (okb) bs_store(o, offb, w[4], w[5], w[6], w[7]);
+    }
+    }  // column window
+}
+
+)");
+    } else if (kPlaneSolve) {
+    std::fprintf(f, "%s", R"(    BS_FENCE();
+    if (it == 0u) __syncthreads();  // mcoef complete
+    // Outputs in groups of R: out = (q row of an erased parity output) + the
+    // sum over syndromes t of c(o, t) * s_t, all in planes.  For each syndrome
+    // the planes y = 2^b * s_t are advanced b = 0..7 (bs_mul2) and XORed into
+    // every output whose coefficient has bit b set (wave-uniform branches).
+#pragma unroll 1
+    for (uint32_t g = 0; g < e; g += R) {
+        uint32_t oid[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            oid[r] = g + r < e ? static_cast<uint32_t>(__builtin_amdgcn_readlane(did_l, g + r)) : 0xFFFFFFFFu;
+        uint32_t out[R][8];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int w = 0; w < 8; ++w) out[r][w] = 0u;
+#pragma unroll
+        for (int t = T0; t < M; ++t) {
+            const int at = 8 * (t - T0);  // row t's accumulators
+            if ((pmask >> t) & 1u) {
+                // Syndrome t's planes enter here (keeps the scheduler from
+                // hoisting every syndrome's advances together).
+                asm volatile("" : "+v"(acc[at + 0]), "+v"(acc[at + 1]), "+v"(acc[at + 2]), "+v"(acc[at + 3]),
+                                  "+v"(acc[at + 4]), "+v"(acc[at + 5]), "+v"(acc[at + 6]), "+v"(acc[at + 7]));
+                // c(g + r, t) for r < R: byte r of one LDS word, made scalar
+                const uint32_t cw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(mcoef[t - T0][g >> 2]));
+                uint32_t y[8];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) y[w] = acc[at + w];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        if ((cw >> (8 * r + b)) & 1u) {
+#pragma unroll
+                            for (int w = 0; w < 8; ++w) out[r][w] ^= y[w];
+                        }
+                    if (b < 7) bs_mul2(y);
+                }
+            }
+            if ((qmask >> t) & 1u) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (oid[r] == static_cast<uint32_t>(K + t)) {
+#pragma unroll
+                        for (int w = 0; w < 8; ++w) out[r][w] ^= acc[at + w];
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                asm volatile("" : "+v"(out[r][0]), "+v"(out[r][1]), "+v"(out[r][2]), "+v"(out[r][3]),
+                                  "+v"(out[r][4]), "+v"(out[r][5]), "+v"(out[r][6]), "+v"(out[r][7])::"memory");
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (g + r >= e) break;
+            bs_from_planes(out[r]);
+            uint8_t* o = shard(oid[r]);
+            if (oka) bs_store(o, offa, out[r][0], out[r][1], out[r][2], out[r][3]);
+            if (okb) bs_store(o, offb, out[r][4], out[r][5], out[r][6], out[r][7]);
+        }
     }
     }  // column window
 }
@@ -746,6 +896,15 @@ int main(int argc, char** argv) {
         argv += 1;
         argc -= 1;
     }
+    for (;;) {  // -S (plane solve), -W / -w (64-bit transpose shifts on / off), -l (no solve tail)
+        if (argc >= 2 && std::string(argv[1]) == "-S") kPlaneSolve = true;
+        else if (argc >= 2 && std::string(argv[1]) == "-W") kShift64 = true;
+        else if (argc >= 2 && std::string(argv[1]) == "-w") kShift64 = false;
+        else if (argc >= 2 && std::string(argv[1]) == "-l") kSolveTail = false;
+        else break;
+        argv += 1;
+        argc -= 1;
+    }
     if (argc >= 3 && std::string(argv[1]) == "-G") {
         kRowGroup = std::atoi(argv[2]);
         if (kRowGroup < 1 || kRowGroup > 16) {
@@ -866,7 +1025,11 @@ int main(int argc, char** argv) {
         argc -= 2;
     }
     if (argc < 3) {
-        std::fprintf(stderr, "usage: %s [-x|-X] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N|-Y] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s [-x|-X] [-S] [-W|-w] [-l] [-G ROWS] [-R OUTPUTS] [-I ITERS] [-T TOPS] [-Q TOP_PREFETCH] [-M] [-B|-Z] [-N|-Y] [-L] [-u] [-E|-e] [-g GEOMETRY] [-p PREFETCH] [-P REC_PREFETCH] OUT.hip K:N [K:N ...]\n", argv[0]);
+        return 2;
+    }
+    if (kPlaneSolve && kRecRows != 4) {
+        std::fprintf(stderr, "the plane solve codes R = 4 outputs per group (-R 4, or -s)\n");
         return 2;
     }
     std::vector<std::pair<int, int>> codes;

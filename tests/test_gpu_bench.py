@@ -37,7 +37,8 @@ def _run(args, env_extra=None, timeout=240):
 @pytest.mark.gpu
 def test_bench_two_ranks_gloo_with_gather_leg(torch_dev):
     d = _run(["--gpus", "2", "--stripes", "64", "--shard", "65536", "--steps", "2", "--warmup", "1",
-              "--cpu-seconds", "0.5", "--gather-stripes", "16", "--gather-timeout", "150"],
+              "--cpu-seconds", "0.5", "--gather-stripes", "16", "--gather-timeout", "150",
+              "--device-set-stripes", "16"],
              {"RSMI_BENCH_BACKEND": "gloo"})
     assert d["n_gpus"] == 2 and len(d["per_rank"]) == 2
     # value = the two ranks' own bytes over the slower rank's time
@@ -52,13 +53,15 @@ def test_bench_two_ranks_gloo_with_gather_leg(torch_dev):
     assert g["verified"]["steps"] == [0, 1]
     assert g["xgmi"]["gathered_GB"] > 0
     assert "communication stream" in g["overlap"]
+    ds = d["device_set"]  # rank 0's device-set context, run between the headline and the gather
+    assert ds["status"] == "ok" and ds["checked"] and ds["spread"]["status"] == "ok", ds
 
 
 @pytest.mark.gpu
 def test_bench_single_gpu_extra_legs(torch_dev):
     d = _run(["--stripes", "64", "--shard", "65536", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.2",
               "--config1-reps", "3", "--config5-stripes", "64", "--config5-steps", "2", "--config5-warmup", "1",
-              "--config3-steps", "2"])
+              "--config3-steps", "2", "--device-set-stripes", "24"])
     assert d["n_gpus"] == 1 and d["roofline"]["frac"] > 0
     assert d["cpu_baseline"] and d["cpu_baseline"]["value"] > 0
     c1 = d["config1"]
@@ -75,3 +78,8 @@ def test_bench_single_gpu_extra_legs(torch_dev):
     c3 = d["config3_worst"]
     assert c3["status"] == "ok", c3
     assert c3["reconstruct"]["bytes"] == 64 * 14 * 65536 and c3["reconstruct"]["GBps"] > 0
+    ds = d["device_set"]
+    assert ds["status"] == "ok" and ds["checked"], ds
+    assert ds["members"] == max(2, ds["members"]) and ds["stripes_per_member"] == 24
+    assert ds["encode"]["GBps"] > 0 and ds["reconstruct"]["GBps"] > 0
+    assert ds["spread"]["status"] == "ok" and ds["spread"]["GBps"] > 0, ds["spread"]
