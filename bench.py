@@ -878,13 +878,18 @@ def main():
     dom_bytes = enc_bytes if do_enc else rec_avg_bytes
     dom_ms = enc_avg_ms if do_enc else rec_avg_ms
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
-    traffic = None
+    # HBM traffic of the dominant kernel: measured by rocprofv3 PMC passes of
+    # this same default line (tools/prof_line.py -> profiles/traffic.json,
+    # keyed by role and workload, naming the profile it came from); the run
+    # itself cannot read counters.
+    traffic = traffic_entry = None
     try:
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        key = f"{dominant}_k{k}_n{n}_S{S}_stripes{stripes}"
-        traffic = tj.get(key)
-    except (OSError, ValueError):
+        traffic_entry = tj.get("entries", {}).get(f"{dominant}_k{k}_n{n}_S{S}_stripes{stripes}")
+        if traffic_entry:
+            traffic = traffic_entry.get("traffic_GB")
+    except (OSError, ValueError, AttributeError):
         pass
 
     out = None
@@ -939,6 +944,11 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": int(dom_bytes),
+                "traffic_source": traffic_entry.get("profile") if traffic_entry else None,
+                "traffic_ratio": traffic_entry.get("traffic_ratio") if traffic_entry else None,
+                "trace_frac": traffic_entry.get("trace_frac") if traffic_entry else None,
+                "note": "achieved/frac: algorithmic bytes / HIP-event time of this run; traffic, traffic_ratio and "
+                        "trace_frac: the rocprofv3 passes of the same default line named by traffic_source",
             },
             "cpu_baseline": cpu,
             "per_rank": [{"rank": r, "ms_per_step": round(v[0] / args.steps * 1e3, 3),

@@ -5,7 +5,13 @@
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
 #if defined(__x86_64__)
 #include <emmintrin.h>
 #endif
@@ -80,6 +86,73 @@ void stage_copy(void* dst, const void* src, size_t n) {
     std::memcpy(dst, src, n);
 }
 
+namespace {
+bool trace_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSMI_TRACE");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+struct TraceCall {
+    std::chrono::steady_clock::time_point t[24];
+    const char* name[24];
+    int n = 0;
+};
+thread_local TraceCall g_call;
+struct TraceTotals {
+    std::mutex mu;
+    std::vector<std::pair<std::string, std::vector<double>>> phases;  // in first-seen order
+    long calls = 0;
+    ~TraceTotals() {
+        if (!calls) return;
+        std::fprintf(stderr, "RSMI_TRACE %ld calls, median / mean us per phase:\n", calls);
+        double total = 0;
+        for (auto& p : phases) {
+            std::vector<double>& v = p.second;
+            double sum = 0;
+            for (double x : v) sum += x;
+            std::sort(v.begin(), v.end());
+            total += v[v.size() / 2];
+            std::fprintf(stderr, "  %-28s %8.2f %8.2f  (%zu)\n", p.first.c_str(), v[v.size() / 2], sum / v.size(),
+                         v.size());
+        }
+        std::fprintf(stderr, "  %-28s %8.2f (sum of medians)\n", "total", total);
+    }
+};
+TraceTotals g_totals;
+}  // namespace
+
+void trace_begin() {
+    if (!trace_on()) return;
+    g_call.n = 0;
+    trace_mark("begin");
+}
+
+void trace_mark(const char* phase) {
+    if (!trace_on() || g_call.n >= 24) return;
+    g_call.t[g_call.n] = std::chrono::steady_clock::now();
+    g_call.name[g_call.n++] = phase;
+}
+
+void trace_end() {
+    if (!trace_on() || g_call.n == 0) return;
+    trace_mark("end");
+    std::lock_guard<std::mutex> lk(g_totals.mu);
+    ++g_totals.calls;
+    for (int i = 1; i < g_call.n; ++i) {
+        const double us = std::chrono::duration<double, std::micro>(g_call.t[i] - g_call.t[i - 1]).count();
+        auto it = std::find_if(g_totals.phases.begin(), g_totals.phases.end(),
+                               [&](const auto& p) { return p.first == g_call.name[i]; });
+        if (it == g_totals.phases.end()) {
+            g_totals.phases.push_back({g_call.name[i], {}});
+            it = g_totals.phases.end() - 1;
+        }
+        it->second.push_back(us);
+    }
+    g_call.n = 0;
+}
+
 void stage_fence() {
 #if defined(__x86_64__)
     if (stage_nt()) _mm_sfence();
@@ -126,10 +199,90 @@ hipError_t wait_event(hipEvent_t ev) {
     return r;
 }
 
+namespace {
+void copy_pieces(const CopyPool::Piece* b, const CopyPool::Piece* e);
+}  // namespace
+
 // ------------------------------------------------------------ CopyPool ----
+struct CopyPool::Async {
+    Job job;
+    bool queued = false;
+};
+
+// Pieces split at kPart and grouped into parts of about group_bytes.
+void CopyPool::split(const std::vector<Piece>& pieces, size_t group_bytes, Job& job) const {
+    size_t group = 0;  // bytes in the part being grouped
+    job.bounds.push_back(0);
+    for (const Piece& p : pieces)
+        for (size_t o = 0; o < p.len; o += kPart) {
+            const size_t len = std::min(kPart, p.len - o);
+            job.pieces.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o, len, p.nt});
+            group += len;
+            if (group >= group_bytes) {
+                job.bounds.push_back(job.pieces.size());
+                group = 0;
+            }
+        }
+    if (job.bounds.back() != job.pieces.size()) job.bounds.push_back(job.pieces.size());
+    job.parts = job.bounds.size() - 1;
+}
+
+CopyPool::Async* CopyPool::start(const std::vector<Piece>& pieces, size_t part_bytes) {
+    Async* a = new (std::nothrow) Async;
+    if (!a) {  // no handle: copy now
+        copy_pieces(pieces.data(), pieces.data() + pieces.size());
+        return nullptr;
+    }
+    split(pieces, std::max<size_t>(part_bytes, 1), a->job);
+    if (a->job.parts == 0) {
+        delete a;
+        return nullptr;
+    }
+    if (threads_.empty()) return a;  // finish() copies it
+    bool wake = false;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        jobs_.push_back(&a->job);
+        a->queued = true;
+        queued_.fetch_add(1, std::memory_order_release);
+        wake = spinners_.load(std::memory_order_acquire) == 0;
+    }
+    if (wake) cv_.notify_one();  // a spinning worker sees queued_ without a wake-up
+    return a;
+}
+
+void CopyPool::finish(Async* a) {
+    if (!a) return;
+    Job& job = a->job;
+    size_t part = 0;
+    if (!a->queued) {
+        while (claim(&job, &part)) copy_part(job, part);
+        delete a;
+        return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    while (claim(&job, &part)) {
+        lk.unlock();
+        copy_part(job, part);
+        lk.lock();
+        ++job.finished;
+    }
+    job.done_cv.wait(lk, [&] { return job.finished == job.parts; });
+    for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
+        if (*it == &job) {
+            jobs_.erase(it);
+            queued_.fetch_sub(1, std::memory_order_release);
+            break;
+        }
+    lk.unlock();
+    delete a;
+}
+
 CopyPool::CopyPool(int threads) {
     const char* e = std::getenv("RSMI_COPY_SPIN_US");
     spin_us_ = e ? std::max(0, std::min(std::atoi(e), 10000)) : 0;
+    const char* ms = std::getenv("RSMI_COPY_SPINNERS");
+    max_spinners_ = ms ? std::max(0, std::atoi(ms)) : 1;
     for (int i = 0; i < threads - 1; ++i) threads_.emplace_back([this] { worker(); });
 }
 
@@ -180,12 +333,16 @@ void CopyPool::worker() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
         if (jobs_.empty() && spin_us_ > 0 && !stop_) {
-            // Out of work: spin a while for the next job before sleeping.
-            lk.unlock();
-            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
-            while (queued_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
-                cpu_relax();
-            lk.lock();
+            // Out of work: spin a while for the next job before sleeping
+            // (at most max_spinners_ workers at once).
+            if (spinners_.fetch_add(1, std::memory_order_acq_rel) < max_spinners_) {
+                lk.unlock();
+                const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+                while (queued_.load(std::memory_order_acquire) == 0 && std::chrono::steady_clock::now() < until)
+                    cpu_relax();
+                lk.lock();
+            }
+            spinners_.fetch_sub(1, std::memory_order_acq_rel);
         }
         cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
         if (stop_) return;
@@ -218,20 +375,7 @@ void CopyPool::run(const std::vector<Piece>& pieces) {
     // Parts of about total / (2 x threads), at least part_min bytes.
     const size_t group_bytes = std::max(part_min, total / (2 * (threads_.size() + 1)));
     Job job;
-    size_t group = 0;  // bytes in the part being grouped
-    job.bounds.push_back(0);
-    for (const Piece& p : pieces)
-        for (size_t o = 0; o < p.len; o += kPart) {
-            const size_t len = std::min(kPart, p.len - o);
-            job.pieces.push_back({static_cast<uint8_t*>(p.dst) + o, static_cast<const uint8_t*>(p.src) + o, len, p.nt});
-            group += len;
-            if (group >= group_bytes) {
-                job.bounds.push_back(job.pieces.size());
-                group = 0;
-            }
-        }
-    if (job.bounds.back() != job.pieces.size()) job.bounds.push_back(job.pieces.size());
-    job.parts = job.bounds.size() - 1;
+    split(pieces, group_bytes, job);
     if (job.parts == 0) return;
     if (threads_.empty() || job.parts == 1) {
         for (size_t i = 0; i < job.parts; ++i) copy_part(job, i);

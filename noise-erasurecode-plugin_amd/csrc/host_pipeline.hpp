@@ -42,9 +42,20 @@ public:
     };
     // Copies every piece (split further into <= 1 MiB parts); returns when done.
     void run(const std::vector<Piece>& pieces);
+    // An asynchronous job: queued for the workers in parts of about
+    // part_bytes, joined by finish(), which copies every part no worker has
+    // claimed yet and waits for the claimed ones -- so a pool whose workers
+    // are asleep costs the caller one wake-up call, and a spinning worker
+    // takes the parts while the caller does other work (a single message's
+    // second staging chunk and present shares, rsmi.cpp decode_launch).
+    struct Async;
+    Async* start(const std::vector<Piece>& pieces, size_t part_bytes);  // nullptr: nothing to copy
+    void finish(Async* a);                                              // joins and frees a
     // Workers that run out of parts spin this long for the next job before
-    // sleeping on the condition variable (RSMI_COPY_SPIN_US, default 0): a
-    // burst of small messages then finds them awake.
+    // sleeping on the condition variable (RSMI_COPY_SPIN_US, default 0), at
+    // most max_spinners of them at once (RSMI_COPY_SPINNERS, default 1): a
+    // stream of messages then finds a helper awake, an idle process burns no
+    // core after the window.
     int spin_us() const { return spin_us_; }
     // The process-wide pool (RSMI_COPY_THREADS workers, default min(8, cpus)).
     static CopyPool& shared();
@@ -69,7 +80,10 @@ private:
     std::condition_variable cv_;
     std::deque<Job*> jobs_;
     std::atomic<int> queued_{0};  // jobs in jobs_ (read without mu_ while spinning)
+    std::atomic<int> spinners_{0};  // workers in their spin window
     int spin_us_ = 0;
+    int max_spinners_ = 1;
+    void split(const std::vector<Piece>& pieces, size_t group_bytes, Job& job) const;
     bool stop_ = false;
 };
 
@@ -85,6 +99,15 @@ hipError_t wait_event(hipEvent_t ev);
 // snoop them out: one config-1 message's kernel reads its 1 MiB 4.7 us faster
 // (tools/stream_probe.hip, profiles/r05j/).  RSMI_STAGE_NT=0: plain memcpy.
 void stage_copy(void* dst, const void* src, size_t n);
+
+// Phase trace of the single-message host calls (RSMI_TRACE=1, diagnostics
+// only; one branch on a static flag otherwise): trace_begin() at a call's
+// entry, trace_mark("name") after each phase, trace_end() at its exit; at
+// process exit the mean microseconds of every phase (time since the previous
+// mark) go to stderr.
+void trace_begin();
+void trace_mark(const char* phase);
+void trace_end();
 // The fence after a run of stage_copy calls (before the launch that reads them).
 void stage_fence();
 

@@ -206,6 +206,14 @@ namespace {
 // stream -- waits for it on the device (begin()), never on the host.
 struct Lease {
     hipStream_t stream = nullptr;  // host API / decode_batch / pattern rows
+    // A single message's odd column chunks (decode_launch, encode_staged) with
+    // RSMI_CHUNK_STREAMS=2: on one stream a chunk's kernel starts 5.4 us after
+    // the previous one ends (profiles/r06h/); on a stream of its own it
+    // overlaps it, but the host copies that run meanwhile slowed 2.5x and the
+    // config-1 decode went 58.0 -> 67.2 us (profiles/r06i/), so one stream is
+    // the default.  Created on first use; joined back into `stream` before the
+    // lease's end().
+    hipStream_t stream2 = nullptr;
     hipEvent_t dev_done = nullptr;
     std::atomic<bool> dev_pending{false};
     hipEvent_t ev[kBatchChunks] = {};  // rs_decode_batch D2H chunk events
@@ -246,7 +254,20 @@ struct Lease {
         if (!pipe) pipe.reset(new (std::nothrow) rsmi::HostPipeline());
         return pipe.get();
     }
+    // The stream of a single message's chunk ch: chunk 0 (and, without a
+    // second stream, every chunk) on `stream`, odd chunks on stream2 when
+    // two streams are in use (RSMI_CHUNK_STREAMS=2).
+    hipStream_t chunk_stream(int ch) {
+        static const bool two = [] {
+            const char* e = std::getenv("RSMI_CHUNK_STREAMS");
+            return e && std::atoi(e) == 2;
+        }();
+        if (!two || ch % 2 == 0) return stream;
+        if (!stream2 && hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) != hipSuccess) stream2 = nullptr;
+        return stream2 ? stream2 : stream;
+    }
     ~Lease() {
+        if (stream2) (void)hipStreamSynchronize(stream2);
         if (stream) (void)hipStreamSynchronize(stream);
         if (dev_pending.load()) (void)hipEventSynchronize(dev_done);
         pipe.reset();
@@ -260,6 +281,7 @@ struct Lease {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         if (dev_done) (void)hipEventDestroy(dev_done);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -1164,14 +1186,29 @@ size_t set_aside_aliases(const OutRanges& out, std::vector<const uint8_t*>& by_i
     return cnt;
 }
 
+// The lease's main stream waits for the chunks launched on stream2 (their
+// events), so L.end(stream) orders the lease's next user after all of them.
+void join_chunks(Lease& L, int launched) {
+    for (int ch = launched - 1; ch >= 0; --ch)
+        if (L.chunk_stream(ch) != L.stream) {
+            (void)hipStreamWaitEvent(L.stream, L.ev[ch], 0);
+            break;  // the last chunk on stream2 follows the earlier ones there
+        }
+}
+
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
 // Rebuild's choice `surv` is read at device address dev[j] (column chunk by
-// column chunk when nch > 1, `stage` filling each chunk's survivor columns
-// first); the present data shares are copied into dst (unless present_done)
-// while the kernel runs (no share overlaps dst: rs_decode set aliasing ones
-// aside).  Returns kDecodeNoStaging, having done nothing, when
-// its pinned staging cannot be had (the caller falls back to the pipeline).
-using StageFn = std::function<void(size_t off, size_t w)>;
+// column chunk when nch > 1, the copies `stage` lists filling each chunk's
+// survivor columns first); the present data shares are copied into dst
+// (unless present_done) while the kernel runs (no share overlaps dst:
+// rs_decode set aliasing ones aside).  Chunk 0 is staged on the calling
+// thread; the later chunks' staging and the present shares are handed to the
+// copy pool at once (async_copies), so a worker awake in its spin window does
+// them while the caller stages chunk 0 and launches -- the caller joins each
+// before it needs it (finish), doing whatever no worker has claimed.
+// Returns kDecodeNoStaging, having done nothing, when its pinned staging
+// cannot be had (the caller falls back to the pipeline).
+using StageFn = std::function<std::vector<rsmi::CopyPool::Piece>(size_t off, size_t w)>;
 constexpr int kDecodeNoStaging = -1000;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
@@ -1241,10 +1278,11 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     std::vector<uint64_t> dev(k);
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
     for (int j = 0; j < k; ++j) dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
-    // survivors' columns [off, off + w) into staging, chunk by chunk
+    // survivors' columns [off, off + w) into staging (non-temporal), chunk by chunk
     auto stage = [&](size_t off, size_t w) {
-        for (int j = 0; j < k; ++j) rsmi::stage_copy(st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w);
-        rsmi::stage_fence();
+        std::vector<rsmi::CopyPool::Piece> v;
+        for (int j = 0; j < k; ++j) v.push_back({st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w, true});
+        return v;
     };
     const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
                                 stage_chunks(static_cast<size_t>(k) * S), stage);
@@ -1262,13 +1300,16 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     for (int i = 0; i < k; ++i)
         if (!present[i]) missing.push_back(i);
     const int e = static_cast<int>(missing.size());
-    auto copy_present = [&] {
-        if (present_done) return;
-        for (int i = 0; i < k; ++i)
-            if (present[i]) std::memmove(dst + static_cast<size_t>(i) * S, by_id[i], S);
+    auto present_pieces = [&] {
+        std::vector<rsmi::CopyPool::Piece> v;
+        if (!present_done)
+            for (int i = 0; i < k; ++i)
+                if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i]) v.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
+        return v;
     };
     if (e == 0) {
-        copy_present();
+        const std::vector<rsmi::CopyPool::Piece> v = present_pieces();
+        rsmi::CopyPool::shared().finish(rsmi::CopyPool::shared().start(v, S));
         return RS_OK;
     }
     // dst never overlaps a share here: rs_decode sets aliasing shares aside
@@ -1292,6 +1333,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     for (int i = 0; i < k; ++i) src[i] = static_cast<uint32_t>(i);
     for (int t = 0; t < e; ++t) dstid[t] = static_cast<uint32_t>(k + t);
     pack_patterns(c, 1, coef.data(), src.data(), dstid.data(), cnt.data(), host);
+    rsmi::trace_mark("rows+pattern");
     void* halias = L.st_onepat.dev;
     uint64_t oalias = 0;
     if (!dst_direct) oalias = reinterpret_cast<uint64_t>(L.st_out.dev);
@@ -1304,12 +1346,47 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     bool strided = !dst_direct;
     for (int jj = 1; jj < k && strided; ++jj) strided = dev[jj] == dev[0] + static_cast<uint64_t>(jj) * span;
     const hipStream_t s = L.stream;
+    rsmi::CopyPool& pool = rsmi::CopyPool::shared();
+    // Helper jobs, oldest first: chunks 1.. of the staging (needed first),
+    // then the present shares.  Parts of ~128 KiB let a worker and the caller
+    // share a job.
+    constexpr size_t kAsyncPart = size_t(128) << 10;
+    // Off by default (RSMI_ASYNC_COPIES=1: on): on the GPU box the helper's
+    // copies slowed the caller's own staging 2.3x (stage0 6.95 -> 16.3 us:
+    // the two threads share the host's copy bandwidth) and the config-1
+    // decode went 56.8 -> 64-66 us (profiles/r06g/).
+    static const bool async_copies = [] {
+        const char* v = std::getenv("RSMI_ASYNC_COPIES");
+        return v && std::atoi(v) != 0;
+    }();
+    std::vector<rsmi::CopyPool::Async*> staged(static_cast<size_t>(nch), nullptr);
+    rsmi::CopyPool::Async* present_job = nullptr;
+    if (async_copies) {
+        if (stage)
+            for (int ch = 1; ch < nch; ++ch) {
+                const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+                staged[ch] = pool.start(stage(off, w), kAsyncPart);
+            }
+        present_job = pool.start(present_pieces(), kAsyncPart);
+    }
     L.begin(s);
+    if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
     hipError_t err = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && err == hipSuccess; ++ch) {
         const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
-        if (stage) stage(off, w);
+        const hipStream_t cs = L.chunk_stream(ch);
+        if (stage) {
+            if (ch > 0 && async_copies) {
+                pool.finish(staged[ch]);
+                staged[ch] = nullptr;
+            } else {
+                const std::vector<rsmi::CopyPool::Piece> v = stage(off, w);
+                for (const rsmi::CopyPool::Piece& q : v) rsmi::stage_copy(q.dst, q.src, q.len);
+                rsmi::stage_fence();
+            }
+        }
+        rsmi::trace_mark(ch ? "stage1" : "stage0");
         rsmi::MatArgs a = strided ? base_args(c, reinterpret_cast<void*>(dev[0] + off), 0,
                                               reinterpret_cast<void*>(oalias + off), 0, span, w, 1)
                                   : base_args(c, nullptr, 0, nullptr, 0, span, w, 1);
@@ -1324,20 +1401,27 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                                         : oalias + static_cast<uint64_t>(t) * span + off;
             a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
         }
-        err = rsmi::launch_matmul(a, e, s);
-        if (err == hipSuccess) err = hipEventRecord(L.ev[ch], s);
+        err = rsmi::launch_matmul(a, e, cs);
+        if (err == hipSuccess) err = hipEventRecord(L.ev[ch], cs);
         if (err == hipSuccess) ++launched;
+        rsmi::trace_mark(ch ? "launch1" : "launch0");
     }
+    join_chunks(L, launched);
     L.end(s);
-    copy_present();  // while the kernel runs
+    for (rsmi::CopyPool::Async* j : staged) pool.finish(j);  // a failed launch left some unjoined
+    if (async_copies) pool.finish(present_job);  // while the kernel runs
+    else pool.finish(pool.start(present_pieces(), S));
+    rsmi::trace_mark("copy_present");
     for (int ch = 0; ch < launched; ++ch) {
         const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
+        rsmi::trace_mark(ch ? "wait1" : "wait0");
         if (err == hipSuccess) err = w8;
         if (err != hipSuccess || dst_direct) continue;
         const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
         for (int t = 0; t < e; ++t)
             std::memcpy(dst + static_cast<size_t>(missing[t]) * S + off,
                         static_cast<uint8_t*>(L.st_out.p) + t * span + off, w);
+        rsmi::trace_mark(ch ? "copyout1" : "copyout0");
     }
     if (launched < nch) (void)rsmi::wait_event(L.dev_done);  // a failed launch: drain what was queued
     return err == hipSuccess ? RS_OK : RS_EDEVICE;
@@ -1356,28 +1440,57 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
     const uint8_t* out = static_cast<const uint8_t*>(L.st_out.p);
     const int nch = std::max(1, std::min(stage_chunks(k * S), static_cast<int>(std::min<size_t>(kBatchChunks, S / 4096))));
     const hipStream_t s = L.stream;
+    // chunk ch's columns of every data shard into staging (non-temporal):
+    // chunk 0 on the calling thread, the others handed to the copy pool at
+    // once and joined before their launch (decode_launch's async_copies)
+    auto pieces = [&](int ch) {
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        std::vector<rsmi::CopyPool::Piece> v;
+        for (size_t j = 0; j < k; ++j) v.push_back({st + j * span + off, input + j * S + off, w, true});
+        return v;
+    };
+    static const bool async_copies = [] {  // off by default, see decode_launch
+        const char* v = std::getenv("RSMI_ASYNC_COPIES");
+        return v && std::atoi(v) != 0;
+    }();
+    rsmi::CopyPool& pool = rsmi::CopyPool::shared();
+    std::vector<rsmi::CopyPool::Async*> staged(static_cast<size_t>(nch), nullptr);
+    if (async_copies)
+        for (int ch = 1; ch < nch; ++ch) staged[ch] = pool.start(pieces(ch), size_t(128) << 10);
     L.begin(s);
+    if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
     hipError_t e = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && e == hipSuccess; ++ch) {
-        // chunk ch's columns of every data shard into staging, then its launch
         const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
-        for (size_t j = 0; j < k; ++j) rsmi::stage_copy(st + j * span + off, input + j * S + off, w);
-        rsmi::stage_fence();
+        const hipStream_t cs = L.chunk_stream(ch);
+        if (staged[ch]) {
+            pool.finish(staged[ch]);
+            staged[ch] = nullptr;
+        } else {
+            for (const rsmi::CopyPool::Piece& q : pieces(ch)) rsmi::stage_copy(q.dst, q.src, q.len);
+            rsmi::stage_fence();
+        }
+        rsmi::trace_mark(ch ? "stage1" : "stage0");
         rsmi::MatArgs a = base_args(c, static_cast<uint8_t*>(din) + off, 0, static_cast<uint8_t*>(dout) + off, 0, span, w, 1);
         set_patterns(c, 1, c->d_encpat.p, a);
         a.stripe_desc = nullptr;
-        e = launch_encode(c, a, s);
-        if (e == hipSuccess) e = hipEventRecord(L.ev[ch], s);
+        e = launch_encode(c, a, cs);
+        if (e == hipSuccess) e = hipEventRecord(L.ev[ch], cs);
         if (e == hipSuccess) ++launched;
+        rsmi::trace_mark(ch ? "launch1" : "launch0");
     }
+    join_chunks(L, launched);
     L.end(s);
+    for (rsmi::CopyPool::Async* j : staged) pool.finish(j);  // a failed launch left some unjoined
     for (int ch = 0; ch < launched; ++ch) {
         const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
+        rsmi::trace_mark(ch ? "wait1" : "wait0");
         if (e == hipSuccess) e = w8;
         if (e != hipSuccess) continue;
         const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
         for (size_t t = 0; t < m; ++t) std::memcpy(parity + t * S + off, out + t * span + off, w);
+        rsmi::trace_mark(ch ? "copyout1" : "copyout0");
     }
     if (launched < nch) (void)rsmi::wait_event(L.dev_done);
     *rc = e == hipSuccess ? RS_OK : RS_EDEVICE;
@@ -2025,6 +2138,10 @@ int rs_reconstruct_ptrs(rs_ctx* c, const uint64_t* shard_ptrs, size_t len, size_
 
 int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     if (!c) return RS_EINVAL;
+    rsmi::trace_begin();
+    struct TraceEnd {
+        ~TraceEnd() { rsmi::trace_end(); }
+    } trace_end_at_exit;
     if (len % static_cast<size_t>(c->k) != 0) return RS_ELEN_NOT_MULTIPLE;
     const size_t S = len / static_cast<size_t>(c->k);
     if (S == 0 || c->m == 0) return RS_OK;
@@ -2037,6 +2154,7 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
     if (!lg.L) return RS_ENOMEM;
+    rsmi::trace_mark("validate+lease");
     int rc_in_place = RS_OK;
     if (encode_in_place(c, *lg.L, input, S, parity, &rc_in_place)) return rc_in_place;
     if (encode_staged(c, *lg.L, input, S, parity, &rc_in_place)) return rc_in_place;
@@ -2057,6 +2175,10 @@ int rs_encode(rs_ctx* c, const uint8_t* input, size_t len, uint8_t* parity) {
 int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t share_len,
               uint8_t* dst) {
     if (!c) return RS_EINVAL;
+    rsmi::trace_begin();
+    struct TraceEnd {
+        ~TraceEnd() { rsmi::trace_end(); }
+    } trace_end_at_exit;
     const int k = c->k, n = c->n;
     if (count < k) return RS_ENOT_ENOUGH;  // Correct: NotEnoughShares comes first
     if (count <= 0) return RS_ENO_SHARES;
@@ -2103,6 +2225,7 @@ int rs_decode(rs_ctx* c, int* numbers, const uint8_t** shares, int count, size_t
     if (!g.ok) return RS_EDEVICE;
     LeaseGuard lg(c);
     if (!lg.L) return RS_ENOMEM;
+    rsmi::trace_mark("validate+lease");
     if (distinct > k) return correct_decode(c, *lg.L, present, by_id, share_len, dst);
     // Survivors in engine-pinned memory (an rs_arena, rs_pinned_alloc): one
     // launch reads them in place, no staging copies.

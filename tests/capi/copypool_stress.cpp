@@ -10,7 +10,8 @@
 // must equal its source byte for byte (starts misaligned on both sides, half
 // the pieces through the non-temporal staging copy, guard bytes untouched);
 // the sanitizers flag any data race on the job queue or out-of-bounds part
-// split or copy.
+// split or copy.  Half the submissions are asynchronous jobs (start /
+// finish, two in flight per caller) with the workers' spin window on or off.
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -48,7 +49,25 @@ int main(int argc, char** argv) {
                     const bool nt = rng() % 2 == 0;  // staging-bound pieces (stage_copy + fence)
                     pieces.push_back({dst[i].data() + doff[i], src[i].data() + soff[i], len, nt});
                 }
-                pool.run(pieces);
+                // Odd iterations go through the asynchronous jobs (start, other
+                // work, finish) that a single message's decode uses: two jobs in
+                // flight at once, joined in either order.
+                if (it % 2 == 0) {
+                    pool.run(pieces);
+                } else {
+                    const size_t half = pieces.size() / 2;
+                    std::vector<rsmi::CopyPool::Piece> a(pieces.begin(), pieces.begin() + half),
+                        b(pieces.begin() + half, pieces.end());
+                    rsmi::CopyPool::Async* ja = pool.start(a, 1 + rng() % (256u << 10));
+                    rsmi::CopyPool::Async* jb = pool.start(b, 1 + rng() % (256u << 10));
+                    if (rng() % 2) {
+                        pool.finish(jb);
+                        pool.finish(ja);
+                    } else {
+                        pool.finish(ja);
+                        pool.finish(jb);
+                    }
+                }
                 for (int i = 0; i < np; ++i) {
                     bool ok = std::equal(src[i].begin() + soff[i], src[i].end(), dst[i].begin() + doff[i]);
                     for (size_t j = 0; j < doff[i]; ++j) ok &= dst[i][j] == 0xA5;

@@ -67,10 +67,16 @@ def test_prof_line_roles_and_traffic(tmp_path):
     md = out.read_text()
     rows = {line.split("|")[1].strip(): line for line in md.splitlines() if line.startswith("| ")}
     assert "2 | 10.000" in rows["headline encode"] and "2 | 9.000" in rows["headline reconstruct"]
-    assert "| 2 |" in rows["config1 (host-API launches: single messages and batches)"]
+    assert "| 2 |" in rows["config1 + device-set launches (host-API messages, members)"]
     assert "config5 encode" in rows and "config5 reconstruct" in rows
-    # encode traffic per launch: (5e6 x 2 + 4e6) KiB = 14.336 GB
-    assert json.loads(traffic.read_text()) == {"encode_k10_n14_S1048576_stripes1": 14.336}
+    # encode traffic per launch: (5e6 x 2 + 4e6) KiB = 14.336 GB, keyed by role and
+    # workload, naming the kernel and the profile it came from
+    tj = json.loads(traffic.read_text())["entries"]
+    enc = tj["encode_k10_n14_S1048576_stripes1"]
+    assert enc["traffic_GB"] == 14.336 and enc["profile"] == str(tmp_path) and "rs_matmul_kernel" in enc["kernel"]
+    assert enc["launches"] == 2 and enc["trace_ms"] == 10.0
+    assert tj["reconstruct_k10_n14_S1048576_stripes1"]["traffic_GB"] == (5e6 * 2 + 2.5e6) * 1024 / 1e9
+    assert set(tj) >= {"config5_encode_k64_n80_S65536_stripes16384", "config5_reconstruct_k64_n80_S65536_stripes16384"}
     assert "| 14.336 |" in rows["headline encode"]
 
 

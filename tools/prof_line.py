@@ -5,12 +5,14 @@ config1 + config5 legs; tools/gpu/r04*.sh layout):
   <dir>/trace/run_kernel_trace.csv   --kernel-trace --stats
   <dir>/fetch/run_counter_collection.csv, <dir>/write/...   --pmc FETCH_SIZE / WRITE_SIZE (optional)
 
-Launches are told apart by kernel and grid size:
-  headline   rs_matmul_kernel launches with the largest grid, in launch order
-             alternating encode / reconstruct (bench.py --mode both);
+Launches are told apart by kernel, grid size and launch order:
+  headline   the first 2 x (warmup + steps) rs_matmul_kernel launches with the
+             largest grid, alternating encode / reconstruct (bench.py --mode
+             both);
+  config3    the later largest-grid launches (the configs[2] worst-case leg:
+             one encode, then its reconstructs);
   config1    the other rs_matmul_kernel launches (the host-API calls on
-             1,048,580-byte messages: one message per launch, and the
-             encode / decode batches' chunk launches);
+             1,048,580-byte messages, the device-set leg's member launches);
   config5    rs_bitslice_k64_m16 (encode) and rs_bitslice_rec_k64_m16
              (reconstruct), invert_patterns_kernel (the fresh patterns).
 HBM traffic per launch = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 (the gfx950
@@ -51,13 +53,18 @@ def short(name):
     return name[:40]
 
 
+HEAD_LAUNCHES = 2 * (3 + 10)  # bench.py defaults: --warmup 3 --steps 10, encode + reconstruct each
+
+
 def roles(trace):
     """{role: [trace rows]} in launch order."""
     mm = [r for r in trace if "rs_matmul_kernel" in r["Kernel_Name"]]
     big = max((grid(r) for r in mm), default=0)
-    head = [r for r in mm if grid(r) == big]
+    top = [r for r in mm if grid(r) == big]
+    head, worst = top[:HEAD_LAUNCHES], top[HEAD_LAUNCHES:]
     out = {"headline encode": head[0::2], "headline reconstruct": head[1::2],
-           "config1 (host-API launches: single messages and batches)": [r for r in mm if grid(r) != big],
+           "config3 worst-case reconstruct": worst[1:],
+           "config1 + device-set launches (host-API messages, members)": [r for r in mm if grid(r) != big],
            "config5 encode": [r for r in trace if "rs_bitslice_k64_m16" in r["Kernel_Name"]],
            "config5 reconstruct": [r for r in trace if "rs_bitslice_rec_k64_m16" in r["Kernel_Name"]],
            "pattern builds": [r for r in trace if "invert_patterns_kernel" in r["Kernel_Name"]]}
@@ -80,7 +87,9 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--bench-json", default=None)
     ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--profile", default=None, help="profile tag / path recorded in each traffic.json entry")
     a = ap.parse_args()
+    a.profile = a.profile or a.dir
     trace = rows(os.path.join(a.dir, "trace", "run_kernel_trace.csv"))
     rl = roles(trace)
     fetch = pmc_by_role(a.dir, "FETCH_SIZE")
@@ -89,7 +98,8 @@ def main():
     # algorithmic bytes per launch
     alg = {"headline encode": 6553 * 14 * (1 << 20),
            "headline reconstruct": 6553 * (10 + 2.5) * (1 << 20),   # E[e] = 2.5 for 1..4 uniform
-           "config1 (host-API launches: single messages and batches)": None,
+           "config3 worst-case reconstruct": 6553 * 14 * (1 << 20),
+           "config1 + device-set launches (host-API messages, members)": None,
            "config5 encode": 16384 * 80 * 65536,
            "config5 reconstruct": 16384 * (64 + 8.5) * 65536}       # E[e] = 8.5 for 1..16 uniform
     if b and "config" in b:
@@ -99,6 +109,8 @@ def main():
     if b and isinstance(b.get("config5"), dict) and b["config5"].get("status") == "ok":
         alg["config5 encode"] = b["config5"]["encode"]["bytes"]
         alg["config5 reconstruct"] = b["config5"]["reconstruct"]["bytes"]
+    if b and isinstance(b.get("config3_worst"), dict) and b["config3_worst"].get("status") == "ok":
+        alg["config3 worst-case reconstruct"] = b["config3_worst"]["reconstruct"]["bytes"]
     lines = [f"# rocprofv3 summary of one bench.py line: {os.path.basename(os.path.normpath(a.dir))}", "",
              "Kernel trace (`--kernel-trace --stats`) plus, when present, separate `--pmc FETCH_SIZE` and "
              "`--pmc WRITE_SIZE` passes of the same command; traffic = FETCH_SIZE x 2 + WRITE_SIZE (gfx950 "
@@ -120,9 +132,23 @@ def main():
                      f"{al / 1e9 if al else float('nan'):.2f} | {ach if ach else float('nan'):.0f} | "
                      f"{ach / 8000 if ach else float('nan'):.4f} | {tr if tr is not None else float('nan'):.3f} | "
                      f"{tr / (al / 1e9) if (tr is not None and al) else float('nan'):.3f} |")
-        if role == "headline encode" and tr is not None and b:
+        # profiles/traffic.json entries (bench.py roofline.traffic / traffic_source),
+        # keyed by role and workload, each naming the kernel and this profile
+        key = {"headline encode": "encode_k10_n14_S1048576_stripes6553",
+               "headline reconstruct": "reconstruct_k10_n14_S1048576_stripes6553",
+               "config3 worst-case reconstruct": "config3_worst_reconstruct_k10_n14_S1048576_stripes6553",
+               "config5 encode": "config5_encode_k64_n80_S65536_stripes16384",
+               "config5 reconstruct": "config5_reconstruct_k64_n80_S65536_stripes16384"}.get(role)
+        if key and b:
             c = b["config"]
-            traffic[f"encode_k{c['k']}_n{c['n']}_S{c['shard_bytes']}_stripes{c['stripes_per_gpu']}"] = round(tr, 3)
+            if role.startswith("headline"):
+                key = f"{role.split()[1]}_k{c['k']}_n{c['n']}_S{c['shard_bytes']}_stripes{c['stripes_per_gpu']}"
+            traffic[key] = {"kernel": kern, "launches": len(d), "trace_ms": round(avg, 3),
+                            "algorithmic_GB": round(al / 1e9, 3) if al else None,
+                            "trace_frac": round(ach / 8000, 4) if ach else None,
+                            "traffic_GB": round(tr, 3) if tr is not None else None,
+                            "traffic_ratio": round(tr / (al / 1e9), 4) if (tr is not None and al) else None,
+                            "profile": a.profile}
     lines.append("")
     stats = rows(os.path.join(a.dir, "trace", "run_kernel_stats.csv"))
     if stats:
@@ -142,9 +168,12 @@ def main():
     with open(a.out, "w") as fh:
         fh.write("\n".join(lines) + "\n")
     if a.traffic_json and traffic:
-        old = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
-        old.update(traffic)
-        json.dump(old, open(a.traffic_json, "w"), indent=1)
+        out = {"_note": "per-launch HBM traffic (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction) and "
+                        "kernel-trace time of each role of one default bench.py line, keyed by role and workload; "
+                        "bench.py copies the entry of its dominant kernel into roofline.traffic / traffic_source. "
+                        "Written by tools/prof_line.py.",
+               "entries": traffic}
+        json.dump(out, open(a.traffic_json, "w"), indent=1)
     print("\n".join(lines))
 
 

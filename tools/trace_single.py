@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Phase trace of one config-1 message's rs_encode / rs_decode (the bench's
+configs[0] calls, pageable buffers, 4 seeded drops): run with RSMI_TRACE=1,
+the engine prints mean microseconds per phase at exit (host_pipeline.cpp
+trace_*).  Usage: RSMI_TRACE=1 python3 tools/trace_single.py {encode|decode} [reps]"""
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "noise-erasurecode-plugin_amd")]
+import numpy as np  # noqa: E402
+
+import rsmi  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+what = sys.argv[1]
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+k, n = 10, 14
+m = n - k
+blob = np.concatenate([oracle.splitmix_bytes(1 << 20, 0x5EED), np.zeros(4, dtype=np.uint8)])
+L = blob.size
+S = L // k
+lib = rsmi.load()
+f = rsmi.FEC(k, n, device=0)
+parity = np.zeros(m * S, dtype=np.uint8)
+P = ctypes.c_void_p
+lib.rs_encode(f.handle, P(blob.ctypes.data), L, P(parity.ctypes.data))
+lost = sorted(int(v) for v in np.random.default_rng(0xC0F1).choice(n, size=4, replace=False))
+keep = [i for i in range(n) if i not in lost]
+bufs = [np.ascontiguousarray(blob[i * S:(i + 1) * S] if i < k else parity[(i - k) * S:(i - k + 1) * S]) for i in keep]
+nums = (ctypes.c_int * k)(*keep)
+ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
+dst = np.zeros(L, dtype=np.uint8)
+bp, pp, dp = P(blob.ctypes.data), P(parity.ctypes.data), P(dst.ctypes.data)
+ts = []
+for _ in range(reps):
+    t0 = time.perf_counter()
+    if what == "encode":
+        lib.rs_encode(f.handle, bp, L, pp)
+    else:
+        lib.rs_decode(f.handle, nums, ptrs, k, S, dp)
+    ts.append(time.perf_counter() - t0)
+if what == "decode":
+    assert np.array_equal(dst, blob)
+print(f"{what}: median {np.median(ts) * 1e6:.1f} us over {reps} calls (dropped {lost})")
