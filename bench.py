@@ -590,6 +590,21 @@ def config1_leg(local, reps=50):
     }
 
 
+def traffic_of(key, path=os.path.join(ROOT, "profiles", "traffic.json")):
+    """{traffic_GB, traffic_ratio, trace_frac, source} of one role in
+    profiles/traffic.json (rocprofv3 passes of the default line,
+    tools/prof_line.py), or None."""
+    try:
+        with open(path) as fh:
+            e = json.load(fh).get("entries", {}).get(key)
+    except (OSError, ValueError, AttributeError):
+        return None
+    if not e:
+        return None
+    return {"traffic_GB": e.get("traffic_GB"), "traffic_ratio": e.get("traffic_ratio"),
+            "trace_frac": e.get("trace_frac"), "source": e.get("profile")}
+
+
 def config3_worst_leg(local, dev, stripes, S, steps=3, warmup=1):
     """configs[2]'s worst case: RS(10,4) with the same
     four data shards (0-3) erased in every stripe, so every stripe
@@ -613,7 +628,8 @@ def config3_worst_leg(local, dev, stripes, S, steps=3, warmup=1):
                 "every stripe (4 regenerated from 6 data + 4 parity)",
         "steps": steps, "warmup": warmup, "stripes": stripes, "shard_bytes": S,
         "reconstruct": {"kernel": f.kernel_name(1), "ms": round(rec_ms, 3), "GBps": round(gbps, 1),
-                        "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes": rec_bytes},
+                        "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes": rec_bytes,
+                        "pmc": traffic_of(f"config3_worst_reconstruct_k{k}_n{n}_S{S}_stripes{stripes}")},
     }
 
 
@@ -645,9 +661,13 @@ def config5_leg(local, dev, stripes=16384, steps=5, warmup=2):
         "ms_per_step": round(run["elapsed"] / steps * 1e3, 3),
         "value_GBps": round((enc_bytes + rec_bytes) / (run["elapsed"] / steps) / 1e9, 1),
         "encode": {"kernel": f.kernel_name(0), "ms": round(enc_ms, 3), "GBps": round(enc_gbps, 1),
-                   "frac": round(enc_gbps / HBM_PEAK_GBS, 4), "bytes": enc_bytes},
+                   "frac": round(enc_gbps / HBM_PEAK_GBS, 4), "bytes": enc_bytes,
+                   "pmc": traffic_of(f"config5_encode_k{k}_n{n}_S{S}_stripes{stripes}")},
         "reconstruct": {"kernel": f.kernel_name(1), "ms": round(rec_ms, 3), "GBps": round(rec_gbps, 1),
-                        "frac": round(rec_gbps / HBM_PEAK_GBS, 4), "bytes": int(rec_bytes)},
+                        "frac": round(rec_gbps / HBM_PEAK_GBS, 4), "bytes": int(rec_bytes),
+                        "pmc": traffic_of(f"config5_reconstruct_k{k}_n{n}_S{S}_stripes{stripes}")},
+        "note": "frac: algorithmic bytes / HIP-event time (incl. the step's fresh-pattern builds for the "
+                "reconstruct); pmc: the rocprofv3 passes of the default line (traffic, trace-based frac, source)",
     }
 
 
