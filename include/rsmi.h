@@ -18,7 +18,8 @@
  *  - Host pointers are never retained past a call (cgo rule).
  *  - Device pointers / streams are HIP device pointers / hipStream_t passed
  *    as void*; the stream may be NULL (legacy default stream).
- *  - An rs_ctx is bound to one HIP device and may be shared between threads
+ *  - An rs_ctx is bound to one HIP device (or to several: a device set,
+ *    rs_new_devices below) and may be shared between threads
  *    (noise calls Receive concurrently, once per peer connection,
  *    main.go:49-52).  Each call leases its own stream, pinned staging and
  *    device workspace from a pool inside the ctx (RSMI_MAX_LEASES, default
@@ -302,7 +303,8 @@ int rs_stream_sync(rs_ctx *ctx, void *stream);
  * A single-device context is a set of one for the calls below. */
 int rs_new_devices(int k, int n, const int *devices, int count, rs_ctx **out);
 int rs_member_count(const rs_ctx *ctx);          /* 1 for a single-device context */
-rs_ctx *rs_member(rs_ctx *ctx, int i);           /* NULL if i is out of range    */
+rs_ctx *rs_member(rs_ctx *ctx, int i);           /* NULL if i is out of range; owned by
+                                                    the set (rs_free on it does nothing) */
 
 /* Contiguous partition of `units` (stripes, messages) into `parts` ranges:
  * part p covers [*first, *first + *count) with first = units*p/parts, so the

@@ -86,7 +86,7 @@ int set_create(int k, int n, const int* devices, int count, DeviceSet** out) {
         rs_ctx* c = nullptr;
         const int st = rs_new_on_device(k, n, devices[i], &c);
         if (st != RS_OK) {
-            for (rs_ctx* m : s->members) rs_free(m);
+            for (rs_ctx* m : s->members) rs_free(m);  // not yet marked as members
             return st;
         }
         s->members.push_back(c);
@@ -128,7 +128,7 @@ int set_create(int k, int n, const int* devices, int count, DeviceSet** out) {
 void set_destroy(DeviceSet* s) {
     if (!s) return;
     s->workers.clear();  // joins: no member work in flight on them
-    for (rs_ctx* m : s->members) rs_free(m);
+    for (rs_ctx* m : s->members) member_free(m);
     delete s;
 }
 

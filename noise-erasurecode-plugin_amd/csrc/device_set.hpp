@@ -26,6 +26,8 @@ struct DeviceSet;
 // distinct member devices.  Returns an rs_status.
 int set_create(int k, int n, const int* devices, int count, DeviceSet** out);
 void set_destroy(DeviceSet* s);
+// Frees a member context (rsmi.cpp; rs_free itself ignores a set's members).
+void member_free(rs_ctx* c);
 
 int set_count(const DeviceSet* s);
 rs_ctx* set_member(const DeviceSet* s, int i);

@@ -295,6 +295,7 @@ struct rs_ctx {
     // every entry point forwards to them (device_set.hpp); nullptr for a
     // single-device context, whose state is everything below.
     rsmi::DeviceSet* set = nullptr;
+    bool set_member = false;  // owned by a device set: rs_free on it is a no-op (the set frees it)
     // Generated bit-sliced encode kernel for this (k, n), if one was built
     // and its embedded matrix equals enc (bitslice.hpp); nullptr otherwise.
     const rsmi::BitsliceKernel* bitslice = nullptr;
@@ -1889,11 +1890,25 @@ int rs_new_devices(int k, int n, const int* devices, int count, rs_ctx** out) {
         delete c;
         return st;
     }
+    for (int i = 0; i < rsmi::set_count(c->set); ++i) rsmi::set_member(c->set, i)->set_member = true;
     *out = c;
     return RS_OK;
 }
 
 int rs_member_count(const rs_ctx* c) { return c ? members_of(c) : RS_EINVAL; }
+
+}  // extern "C"
+
+namespace rsmi {
+// device_set.cpp: frees a member context (rs_free ignores members).
+void member_free(rs_ctx* c) {
+    if (!c) return;
+    c->set_member = false;
+    rs_free(c);
+}
+}  // namespace rsmi
+
+extern "C" {
 
 rs_ctx* rs_member(rs_ctx* c, int i) { return c ? member_of(c, i) : nullptr; }
 
@@ -1910,7 +1925,7 @@ int rs_partition(size_t units, int parts, int part, size_t* first, size_t* count
 }
 
 void rs_free(rs_ctx* c) {
-    if (!c) return;
+    if (!c || c->set_member) return;  // a set's member (rs_member) is freed with its set
     if (c->set) {
         rsmi::set_destroy(c->set);
         delete c;

@@ -237,6 +237,11 @@ def test_set_routes_device_resident_calls_by_buffer():
     assert torch.equal(data, d0)
     f.prepare_patterns(2)  # every member
     assert f.pattern_count() >= 2 * (n + n * (n - 1) // 2)
+    # a member belongs to its set: rs_free on it does nothing, the set still works
+    rsmi.load().rs_free(f.member(1).handle)
+    msgs = _config1_messages(k, n, 4096, 4, 3)
+    pars, st = f.EncodeBatch([d for d, _, _ in msgs])
+    assert st == [0] * 4 and pars == [p for _, p, _ in msgs]
     f.close()
     with pytest.raises(rsmi.RSError) as ei:
         rsmi.FEC(k, n, devices=[0, torch.cuda.device_count() + 7])

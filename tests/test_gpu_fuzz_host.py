@@ -24,3 +24,4 @@ def test_host_api_random_cases(seed):
     st = fuzz_host_api.run(cases=60, seed=seed)
     assert st["failures"] == 0, st["first_failures"]
     assert st["encode"] == 60 and st["decode_k"] + st["decode_more"] == 60
+    assert st["aliased"] > 0  # shares inside dst (round 6)

@@ -353,7 +353,7 @@ def test_mask_diagnostic_build(tmp_path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     lib = os.path.join(root, "noise-erasurecode-plugin_amd", "lib_diag", "librsmi.so")
-    assert os.path.exists(lib), "lib_diag/librsmi.so is built by the Makefile (build())"
+    assert os.path.exists(lib), "lib_diag/librsmi.so is built by `make diag` (build())"
     k, n = 64, 80
     er = np.concatenate([_fixed_patterns(k, n), _erasures(np.random.default_rng(16), 512, n, n - k)])
     np.save(tmp_path / "er.npy", er)

@@ -7,7 +7,11 @@ one corrupted share (Correct / Berlekamp-Welch), survivors in pageable
 memory, in an engine-pinned rs_arena (read in place) or mixed, dst pageable
 or engine-pinned.  Every fourth case also runs a batch of 1-40 messages of
 that shape through rs_encode_batch and rs_decode_batch (own shares, drops,
-corruptions and survivor placement per message).  Every parity and every
+corruptions and survivor placement per message).  Aliasing (infectious lets
+Decode's shares alias dst; round 6): some single decodes put every share and
+dst in one buffer (rows in a random order, dst at a random row and byte
+shift, pinned or pageable), and some batches put each message's shares in a
+block that its own or the next message's dst covers.  Every parity and every
 decoded message is compared with the oracle's.  Prints one JSON line.
 
 usage: tools/fuzz_host_api.py [--seconds 120 | --cases N] [--seed 1]
@@ -47,6 +51,20 @@ def batch_case(rng, lib, f, E, k, n, S, stats, oracle, rsmi):
     counts, nums, ptrs, keep, refs, arenas = [], [], [], [], [], []
     in_arena = rng.random() < 0.4
     arena = rsmi.Arena(B * n * (S + 256) + 4096) if in_arena else None
+    # aliasing: message b's shares in rows of block b, its dst in block (b + off) % B
+    alias = not in_arena and rng.random() < 0.15
+    rows = n + 2
+    blk_bytes = rows * S + S
+    blk_pinned = alias and rng.random() < 0.5
+    blk_keep = None
+    if alias:
+        if blk_pinned:
+            base = lib.rs_pinned_alloc(B * blk_bytes)
+        else:
+            blk_keep = np.zeros(B * blk_bytes, dtype=np.uint8)
+            base = blk_keep.ctypes.data
+        off = int(rng.integers(0, 2))
+        shift = int(rng.integers(0, S)) if rng.random() < 0.5 else 0
     for b in range(B):
         cnt = k if rng.random() < 0.7 else int(rng.integers(k, n + 1))
         ids = [int(v) for v in rng.choice(n, size=cnt, replace=False)]
@@ -57,27 +75,40 @@ def batch_case(rng, lib, f, E, k, n, S, stats, oracle, rsmi):
         shares = [(i, sh[i].tobytes()) for i in ids]
         refs.append(oracle.decode(E, k, n, shares) if cnt == k else oracle.decode_correct(E, k, n, shares))
         counts.append(cnt)
-        for i in ids:
+        perm = rng.permutation(rows)
+        for j, i in enumerate(ids):
             nums.append(i)
-            if arena is not None:
+            if alias:
+                a = base + b * blk_bytes + int(perm[j]) * S
+                ctypes.memmove(a, sh[i].tobytes(), S)
+                ptrs.append(a)
+            elif arena is not None:
                 ptrs.append(arena.put(sh[i].tobytes()))
             else:
                 keep.append(sh[i])
                 ptrs.append(sh[i].ctypes.data)
     dsts = [np.zeros(k * S, dtype=np.uint8) for _ in range(B)]
+    dptr = ([base + ((b + off) % B) * blk_bytes + shift for b in range(B)] if alias
+            else [d.ctypes.data for d in dsts])
     cc = (ctypes.c_int * B)(*counts)
     nn = (ctypes.c_int * len(nums))(*nums)
     pp = (ctypes.c_void_p * len(ptrs))(*ptrs)
-    dd = (ctypes.c_void_p * B)(*[d.ctypes.data for d in dsts])
+    dd = (ctypes.c_void_p * B)(*dptr)
     st = (ctypes.c_int * B)()
     lib.rs_decode_batch(f.handle, B, cc, nn, pp, S, dd, st)
+    if alias:
+        for b in range(B):
+            dsts[b][:] = np.frombuffer(ctypes.string_at(dptr[b], k * S), dtype=np.uint8)
+        if blk_pinned:
+            lib.rs_pinned_free(base)
+        stats["aliased_batch_msgs"] += B
     if arena is not None:
         arena.free()
     for b in range(B):
         ref_rc, ref = refs[b]
-        assert (st[b] == 0) == (ref_rc == 0), f"k={k} n={n} S={S} B={B} decode_batch msg {b} rc {st[b]} vs {ref_rc}"
+        assert (st[b] == 0) == (ref_rc == 0), f"k={k} n={n} S={S} B={B} alias={alias} decode_batch msg {b} rc {st[b]} vs {ref_rc}"
         if st[b] == 0:
-            assert dsts[b].tobytes() == ref == datas[b].tobytes(), f"k={k} n={n} S={S} B={B} decode_batch msg {b} bytes"
+            assert dsts[b].tobytes() == ref == datas[b].tobytes(), f"k={k} n={n} S={S} B={B} alias={alias} decode_batch msg {b} bytes"
     stats["decode_batch_msgs"] += B
 
 
@@ -90,7 +121,8 @@ def run(seconds=None, cases=None, seed=1):
     P = ctypes.c_void_p
     fecs, mats = {}, {}
     stats = {"cases": 0, "encode": 0, "decode_k": 0, "decode_more": 0, "corrupted": 0, "arena": 0,
-             "pinned_dst": 0, "encode_batch_msgs": 0, "decode_batch_msgs": 0, "failures": 0}
+             "pinned_dst": 0, "aliased": 0, "encode_batch_msgs": 0, "decode_batch_msgs": 0,
+             "aliased_batch_msgs": 0, "failures": 0}
     first = []
     t0 = last_note = time.time()
     while (cases is None or stats["cases"] < cases) and (seconds is None or time.time() - t0 < seconds):
@@ -129,7 +161,25 @@ def run(seconds=None, cases=None, seed=1):
             where = rng.random()
             arena = None
             ptr = {}
-            if where < 0.35:  # every survivor in an engine-pinned arena slot
+            # aliasing: the shares and dst in one buffer (random rows, dst at a
+            # random row and byte shift), pinned or pageable
+            alias = rng.random() < 0.15
+            alias_keep = alias_pinned = None
+            if alias:
+                rows = n + 2
+                size = rows * S + S
+                alias_pinned = rng.random() < 0.5
+                if alias_pinned:
+                    blk = lib.rs_pinned_alloc(size)
+                else:
+                    alias_keep = np.zeros(size, dtype=np.uint8)
+                    blk = alias_keep.ctypes.data
+                perm = rng.permutation(rows)
+                for j, i in enumerate(ids):
+                    ptr[i] = blk + int(perm[j]) * S
+                    ctypes.memmove(ptr[i], bufs[i].tobytes(), S)
+                stats["aliased"] += 1
+            elif where < 0.35:  # every survivor in an engine-pinned arena slot
                 arena = rsmi.Arena(sum(S + 256 for _ in ids) + 4096)
                 for i in ids:
                     ptr[i] = arena.put(bufs[i].tobytes())
@@ -141,8 +191,11 @@ def run(seconds=None, cases=None, seed=1):
             else:
                 for i in ids:
                     ptr[i] = bufs[i].ctypes.data
-            pinned_dst = rng.random() < 0.25
-            if pinned_dst:
+            pinned_dst = not alias and rng.random() < 0.25
+            if alias:
+                drow = int(rng.integers(0, rows - k + 1))
+                dp = blk + drow * S + (int(rng.integers(0, S)) if rng.random() < 0.5 else 0)
+            elif pinned_dst:
                 dp = lib.rs_pinned_alloc(max(k * S, 16))
                 ctypes.memset(dp, 0, max(k * S, 16))
                 stats["pinned_dst"] += 1
@@ -162,8 +215,11 @@ def run(seconds=None, cases=None, seed=1):
                 stats["decode_more"] += 1
             if pinned_dst:
                 lib.rs_pinned_free(dp)
+            if alias_pinned:
+                lib.rs_pinned_free(blk)
             if arena is not None:
                 arena.free()
+            case += f" alias={alias}"
             assert (rc == 0) == (ref_rc == 0), f"{case} cnt={cnt} corrupt={corrupt} rc {rc} vs oracle {ref_rc}"
             if rc == 0:
                 assert got == ref, f"{case} cnt={cnt} corrupt={corrupt} decode bytes"
