@@ -98,8 +98,10 @@ def parse():
                     help="seconds after which a stuck gather leg is abandoned (the line is still printed, "
                          f"then the ranks exit {EXIT_GATHER_ABANDONED})")
     ap.add_argument("--device-set-stripes", type=int, default=512,
-                    help="stripes per member of the device-set leg (rank 0: one rs_new_devices context over every "
-                         "visible GPU, [0, 0] on a one-GPU box; never value); 0 skips")
+                    help="N = 1: stripes per member of the device-set leg (a child process: one rs_new_devices "
+                         "context over every visible GPU, [0, 0] on a one-GPU box; never value); 0 skips")
+    ap.add_argument("--device-set-timeout", type=float, default=240.0)
+    ap.add_argument("--device-set-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
                     help="N = 1: skip the configs[0] (per-message latency), configs[4] (RS(64,16)) and "
                          "configs[2] worst-case legs reported beside the headline")
@@ -818,9 +820,29 @@ def device_set_leg(k, n, S, stripes, steps=3, warmup=1, spread_stripes=256, seed
     return out
 
 
+def device_set_child(args, k, n, S):
+    """device_set_leg in a child process (bench.py --device-set-child), its
+    JSON relayed; a failure, crash or timeout becomes the leg's status."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--device-set-child", "--k", str(k), "--n", str(n),
+           "--shard", str(S), "--device-set-stripes", str(args.device_set_stripes)]
+    try:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           timeout=args.device_set_timeout)
+    except subprocess.TimeoutExpired:
+        return {"status": f"error: device-set child timed out after {args.device_set_timeout} s"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.lstrip().startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"status": f"error: device-set child exited {p.returncode}: {p.stderr[-400:]}"}
+    return json.loads(lines[-1])
+
+
 def main():
     global _RESULT_OUT
     args = parse()
+    if args.device_set_child:  # bench.py's own child (device_set_child): one JSON line, nothing else
+        print(json.dumps(guarded_leg(lambda: device_set_leg(args.k, args.n, args.shard, args.device_set_stripes))))
+        return
     how = check_world(args.gpus)
     if how == "launch":
         sys.exit(self_launch(args.gpus, sys.argv[1:]))
@@ -976,15 +998,14 @@ def main():
                           "encode_ms": round(v[1], 3), "reconstruct_ms": round(v[2], 3)}
                          for r, v in enumerate(per_rank)],
         }
-    if args.device_set_stripes > 0 and (world > 1 or args.extra_legs):
-        # The device-set context over every GPU this process sees, run by rank
-        # 0 alone while the other ranks wait (after the headline is measured).
+    if args.device_set_stripes > 0 and world == 1 and args.extra_legs:
+        # The device-set context over every GPU a process sees (N = 1 only:
+        # all of a node's GPUs are visible to it), in a child process, so a
+        # fault or hang there (its peer reads have never run on an 8-GPU
+        # node here) cannot cost the headline line.
         del f
         torch.cuda.empty_cache()
-        if rank == 0:
-            out["device_set"] = guarded_leg(lambda: device_set_leg(k, n, S, args.device_set_stripes))
-        if distributed:
-            torch.distributed.barrier()
+        out["device_set"] = device_set_child(args, k, n, S)
         f = rsmi.FEC(k, n, device=local)
     if distributed and world > 1 and args.gather_stripes > 0:
         # configs[3]'s survivor gather on the same ranks, after the headline

@@ -1187,6 +1187,19 @@ size_t set_aside_aliases(const OutRanges& out, std::vector<const uint8_t*>& by_i
     return cnt;
 }
 
+// Whether each column chunk of a single message records its own event
+// (default: chunk c's rows are copied out while chunk c + 1 codes);
+// RSMI_CHUNK_EVENTS=0 records only the last chunk's and copies every chunk
+// out after it (A/B: whether the marker between the two kernels costs the
+// 5.4-us gap of profiles/r06h/).
+bool chunk_events() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSMI_CHUNK_EVENTS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 // The lease's main stream waits for the chunks launched on stream2 (their
 // events), so L.end(stream) orders the lease's next user after all of them.
 void join_chunks(Lease& L, int launched) {
@@ -1372,6 +1385,8 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     }
     L.begin(s);
     if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
+    // every chunk records its event unless RSMI_CHUNK_EVENTS=0 on one stream
+    const bool ev_each = chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t err = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && err == hipSuccess; ++ch) {
@@ -1403,7 +1418,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
             a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
         }
         err = rsmi::launch_matmul(a, e, cs);
-        if (err == hipSuccess) err = hipEventRecord(L.ev[ch], cs);
+        if (err == hipSuccess && (ev_each || ch == nch - 1)) err = hipEventRecord(L.ev[ch], cs);
         if (err == hipSuccess) ++launched;
         rsmi::trace_mark(ch ? "launch1" : "launch0");
     }
@@ -1414,11 +1429,13 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     else pool.finish(pool.start(present_pieces(), S));
     rsmi::trace_mark("copy_present");
     for (int ch = 0; ch < launched; ++ch) {
+        if (!ev_each && ch < nch - 1) continue;  // no event of its own: copied out with the last chunk
         const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
         rsmi::trace_mark(ch ? "wait1" : "wait0");
         if (err == hipSuccess) err = w8;
         if (err != hipSuccess || dst_direct) continue;
-        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        const int c0 = ev_each ? ch : 0;  // chunks [c0, ch] copied out now
+        const size_t off = chunk_off(S, c0, nch), w = chunk_off(S, ch + 1, nch) - off;
         for (int t = 0; t < e; ++t)
             std::memcpy(dst + static_cast<size_t>(missing[t]) * S + off,
                         static_cast<uint8_t*>(L.st_out.p) + t * span + off, w);
@@ -1460,6 +1477,7 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
         for (int ch = 1; ch < nch; ++ch) staged[ch] = pool.start(pieces(ch), size_t(128) << 10);
     L.begin(s);
     if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
+    const bool ev_each = chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t e = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && e == hipSuccess; ++ch) {
@@ -1477,7 +1495,7 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
         set_patterns(c, 1, c->d_encpat.p, a);
         a.stripe_desc = nullptr;
         e = launch_encode(c, a, cs);
-        if (e == hipSuccess) e = hipEventRecord(L.ev[ch], cs);
+        if (e == hipSuccess && (ev_each || ch == nch - 1)) e = hipEventRecord(L.ev[ch], cs);
         if (e == hipSuccess) ++launched;
         rsmi::trace_mark(ch ? "launch1" : "launch0");
     }
@@ -1485,11 +1503,13 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
     L.end(s);
     for (rsmi::CopyPool::Async* j : staged) pool.finish(j);  // a failed launch left some unjoined
     for (int ch = 0; ch < launched; ++ch) {
+        if (!ev_each && ch < nch - 1) continue;  // copied out with the last chunk
         const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
         rsmi::trace_mark(ch ? "wait1" : "wait0");
         if (e == hipSuccess) e = w8;
         if (e != hipSuccess) continue;
-        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        const int c0 = ev_each ? ch : 0;
+        const size_t off = chunk_off(S, c0, nch), w = chunk_off(S, ch + 1, nch) - off;
         for (size_t t = 0; t < m; ++t) std::memcpy(parity + t * S + off, out + t * span + off, w);
         rsmi::trace_mark(ch ? "copyout1" : "copyout0");
     }
