@@ -2297,6 +2297,10 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
                     size_t S, uint8_t** dsts, int* status) {
     if (!c || batch < 0 || (batch && (!counts || !numbers || !shares || !dsts || !status)))
         return RS_EINVAL;
+    rsmi::trace_begin();
+    struct TraceEnd {
+        ~TraceEnd() { rsmi::trace_end(); }
+    } trace_end_at_exit;
     if (c->set) return rsmi::set_decode_batch(c->set, batch, counts, numbers, shares, S, dsts, status);
     const int k = c->k, n = c->n;
     if (batch > 0 && S > 0) {
@@ -2536,22 +2540,32 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
                 rows_before[j + 1] = rows_before[j] + e_j;
             }
             size_t launched = 0;
+            static const char* const kStage[] = {"stage0", "stage1", "stage2", "stage3"};
+            static const char* const kLaunch[] = {"launch0", "launch1", "launch2", "launch3"};
+            static const char* const kWait[] = {"wait0", "wait1", "wait2", "wait3"};
+            static const char* const kOut[] = {"copyout0", "copyout1", "copyout2", "copyout3"};
+            static_assert(kBatchChunks == 4, "trace phase names");
             for (size_t ch = 0; ch < nch; ++ch) {
                 const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
                 if (!in_place)
                     pipe->copy(std::vector<rsmi::CopyPool::Piece>(stage_in.begin() + j0 * k, stage_in.begin() + j1 * k));
+                rsmi::trace_mark(kStage[ch]);
                 const int st = reconstruct(c, L, nullptr, 0, nullptr, 0, sp, S, j1 - j0, erased.data() + j0 * n,
                                            static_cast<const uint64_t*>(L.d_pieces.p) + j0 * n, s);
                 if (st != RS_OK || hipEventRecord(L.ev[ch], s) != hipSuccess) return finish(st != RS_OK ? st : RS_EDEVICE);
+                rsmi::trace_mark(kLaunch[ch]);
                 ++launched;
             }
             pipe->copy(direct);  // present data shards: no GPU, while it works
+            rsmi::trace_mark("copy_present");
             for (size_t ch = 0; ch < launched; ++ch) {
                 if (rsmi::wait_event(L.ev[ch]) != hipSuccess) return finish(RS_EDEVICE);
+                rsmi::trace_mark(kWait[ch]);
                 const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
                 std::vector<rsmi::CopyPool::Piece> out;
                 for (size_t r = rows_before[j0]; r < rows_before[j1]; ++r) out.push_back({regen[r], h_out + r * sp, S});
                 pipe->copy(out);
+                rsmi::trace_mark(kOut[ch]);
             }
             return RS_OK;
         }
@@ -2651,6 +2665,10 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
 int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t len, uint8_t* const* parities,
                     int* status) {
     if (!c || batch < 0 || (batch && (!inputs || !parities || !status))) return RS_EINVAL;
+    rsmi::trace_begin();
+    struct TraceEnd {
+        ~TraceEnd() { rsmi::trace_end(); }
+    } trace_end_at_exit;
     if (c->set) return rsmi::set_encode_batch(c->set, batch, inputs, len, parities, status);
     const size_t k = static_cast<size_t>(c->k), m = static_cast<size_t>(c->m);
     if (len % k != 0) {
@@ -2721,6 +2739,7 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
                 for (size_t i = 0; i < k; ++i)
                     in.push_back({h_in + (j * k + i) * pitch, inputs[todo[g0 + j]] + i * S, S, true});
             pipe->copy(in);
+            rsmi::trace_mark(ch == 0 ? "stage0" : ch == 1 ? "stage1" : ch == 2 ? "stage2" : "stage3");
             rsmi::MatArgs a = base_args(c, d_in + j0 * k * pitch, k * pitch, d_out + j0 * m * pitch, m * pitch, pitch, S,
                                         j1 - j0);
             set_patterns(c, 1, c->d_encpat.p, a);
@@ -2728,10 +2747,12 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
             e = launch_encode(c, a, s);
             if (e == hipSuccess) e = hipEventRecord(L.ev[ch], s);
             if (e == hipSuccess) ++launched;
+            rsmi::trace_mark(ch == 0 ? "launch0" : ch == 1 ? "launch1" : ch == 2 ? "launch2" : "launch3");
         }
         L.end(s);
         for (size_t ch = 0; ch < launched && e == hipSuccess; ++ch) {
             e = rsmi::wait_event(L.ev[ch]);
+            rsmi::trace_mark(ch == 0 ? "wait0" : ch == 1 ? "wait1" : ch == 2 ? "wait2" : "wait3");
             if (e != hipSuccess) break;
             const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
             std::vector<rsmi::CopyPool::Piece> out;
@@ -2739,6 +2760,7 @@ int rs_encode_batch(rs_ctx* c, int batch, const uint8_t* const* inputs, size_t l
             for (size_t j = j0; j < j1; ++j)
                 for (size_t t = 0; t < m; ++t) out.push_back({parities[todo[g0 + j]] + t * S, h_out + (j * m + t) * pitch, S});
             pipe->copy(out);
+            rsmi::trace_mark(ch == 0 ? "copyout0" : ch == 1 ? "copyout1" : ch == 2 ? "copyout2" : "copyout3");
         }
         if (e != hipSuccess) {
             (void)hipStreamSynchronize(s);  // nothing may still read the staging

@@ -12,7 +12,11 @@ for mode in 1 0; do
   done
 done
 done
+for w in encode_batch decode_batch; do
+  RSMI_TRACE=1 timeout -k 10 120 python3 tools/trace_single.py $w 400 > $O/$w.trace 2>&1 || exit 5
+done
 grep -H "median" $O/*.trace | grep -v RSMI
+cat $O/encode_batch.trace $O/decode_batch.trace
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_device_set.py tests/test_gpu_fuzz_host.py tests/test_capi_c.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 RSMI_CHUNK_EVENTS=0 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_plugin.py -m gpu -x -q -k "decode or encode" --timeout 300 --timeout-method thread > $O/pytest_ev0.log 2>&1 || { tail -30 $O/pytest_ev0.log; exit 3; }

@@ -15,7 +15,7 @@ import numpy as np  # noqa: E402
 import rsmi  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-what = sys.argv[1]
+what = sys.argv[1]  # encode | decode | encode_batch | decode_batch (64 messages per call)
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
 k, n = 10, 14
 m = n - k
@@ -34,14 +34,38 @@ nums = (ctypes.c_int * k)(*keep)
 ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
 dst = np.zeros(L, dtype=np.uint8)
 bp, pp, dp = P(blob.ctypes.data), P(parity.ctypes.data), P(dst.ctypes.data)
+B = 64
+if what.endswith("batch"):
+    reps = max(5, reps // 20)
+    rng = np.random.default_rng(0xBA7C)
+    bkeeps = [sorted(set(range(n)) - set(int(v) for v in rng.choice(n, size=4, replace=False))) for _ in range(B)]
+    base = {i: (blob.ctypes.data + i * S if i < k else parity.ctypes.data + (i - k) * S) for i in range(n)}
+    bdst = [np.zeros(L, dtype=np.uint8) for _ in range(B)]
+    bcounts = (ctypes.c_int * B)(*[k] * B)
+    bnums = (ctypes.c_int * (B * k))(*[i for kp in bkeeps for i in kp])
+    bptrs = (ctypes.c_void_p * (B * k))(*[base[i] for kp in bkeeps for i in kp])
+    bout = (ctypes.c_void_p * B)(*[d.ctypes.data for d in bdst])
+    emsgs = [np.ascontiguousarray(np.roll(blob, 4099 * b)) for b in range(B)]
+    epar = [np.zeros(m * S, dtype=np.uint8) for _ in range(B)]
+    eins = (ctypes.c_void_p * B)(*[x.ctypes.data for x in emsgs])
+    eout = (ctypes.c_void_p * B)(*[x.ctypes.data for x in epar])
+    bst = (ctypes.c_int * B)()
 ts = []
 for _ in range(reps):
     t0 = time.perf_counter()
     if what == "encode":
         lib.rs_encode(f.handle, bp, L, pp)
-    else:
+    elif what == "decode":
         lib.rs_decode(f.handle, nums, ptrs, k, S, dp)
+    elif what == "encode_batch":
+        lib.rs_encode_batch(f.handle, B, eins, L, eout, bst)
+    else:
+        lib.rs_decode_batch(f.handle, B, bcounts, bnums, bptrs, S, bout, bst)
     ts.append(time.perf_counter() - t0)
 if what == "decode":
     assert np.array_equal(dst, blob)
-print(f"{what}: median {np.median(ts) * 1e6:.1f} us over {reps} calls (dropped {lost})")
+if what == "decode_batch":
+    assert all(np.array_equal(d, blob) for d in bdst)
+per = B if what.endswith("batch") else 1
+print(f"{what}: median {np.median(ts) * 1e6:.1f} us over {reps} calls ({np.median(ts) * 1e6 / per:.1f} us per message; "
+      f"single-message drops {lost})")
