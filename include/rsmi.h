@@ -196,6 +196,8 @@ enum {
     RS_STAT_REC_STRIPES_TABLE = 7,  /* stripes reconstructed by the split-table kernel (batched API) */
     RS_STAT_REC_STRIPES_SYNDROME = 8, /* ... by the bit-sliced syndrome kernels                     */
     RS_STAT_ENCODE_BATCHES = 9,    /* rs_encode_batch GPU passes (one per staging group) */
+    RS_STAT_MAILBOX_CALLS = 10,    /* rs_encode / rs_decode calls whose chunks went to a mailbox grid */
+    RS_STAT_MAILBOX_RECOVERED = 11, /* ... of them with a chunk the grid left undone (launched by the caller) */
 };
 int64_t rs_stat(const rs_ctx *ctx, int which);
 

@@ -125,9 +125,11 @@ __device__ __forceinline__ void step_fence(uint32_t (&acc)[kRowsPerStep][4]) {
 }
 
 // One block codes a chunk of 16-byte columns of one stripe for one group of
-// MG output rows.  LDS: [k][MG/4][20] table dwords | k survivor pointers.
+// MG output rows: logical block `blk` of `nblk` (rs_matmul_kernel: blockIdx.x
+// of the grid; rs_resident_kernel: each job's blocks in turn).  LDS: [k][MG/4][20]
+// table dwords | k survivor pointers.
 template <int K, int MG, int BT, bool NT>
-__global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
+__device__ __forceinline__ void matmul_block(const MatArgs& a, uint32_t blk, uint32_t nblk, uint4* lds4) {
     static_assert(MG % 2 == 0, "MG must be even");
     constexpr int TG = (MG + kRowsPerStep - 1) / kRowsPerStep;  // sub-steps per survivor
     constexpr int RL = MG - (TG - 1) * kRowsPerStep;            // rows in the last sub-step
@@ -143,12 +145,11 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
 #endif
     constexpr int JB = (K == 0) ? 8 : (K <= 16 ? K : 8);  // survivor loads in flight
     const int k = K ? K : static_cast<int>(a.k);
-    extern __shared__ uint4 lds4[];
     uint32_t* tw = reinterpret_cast<uint32_t*>(lds4);
     uint8_t** sptr = reinterpret_cast<uint8_t**>(tw + k * MG * 5);
 
     // XCD-aware order (xcd.hpp): regions of a.xcd blocks per XCD in turn.
-    uint64_t b = a.xcd ? xcd_block(blockIdx.x, a.xcd, gridDim.x) : blockIdx.x;
+    uint64_t b = a.xcd ? xcd_block(blk, a.xcd, nblk) : blk;
     const uint32_t grp = static_cast<uint32_t>(b % a.groups);
     b /= a.groups;
     const uint32_t chunk = static_cast<uint32_t>(b % a.chunks);
@@ -349,6 +350,114 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
     }
 }
 
+template <int K, int MG, int BT, bool NT>
+__global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
+    extern __shared__ uint4 lds4[];
+    matmul_block<K, MG, BT, NT>(a, blockIdx.x, gridDim.x, lds4);
+}
+
+// ------------------------------------------------------------- mailbox --
+// One grid per single-message call (rs_kernels.hpp MailboxHost): block 0
+// polls `posted` over PCIe and hands each job to the grid through
+// MailboxDev::go; every block codes its share of the job's logical blocks
+// and the last one to finish writes done[j - 1].  A call's chunks then cost
+// the host a 0.3 KiB write each instead of a launch and an event, and the
+// grid's dispatch overlaps the staging of the first chunk (profiles/r06h/:
+// 4.3 us to launch a chunk, 5 us to dispatch it, 5.4 us between two
+// chunks' kernels).  Every wave leaves: after the last job, on quit, or on
+// a timeout.
+__device__ __forceinline__ uint64_t mb_clock() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <int K, int MG, int BT>
+__global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxDev* d, uint32_t njobs,
+                                                        uint64_t timeout) {
+    extern __shared__ uint4 lds4[];
+    __shared__ MailboxJob job;
+    __shared__ uint64_t go_s;
+    for (uint32_t cur = 1; cur <= njobs; ++cur) {
+        if (threadIdx.x == 0) {
+            uint64_t g;
+            const uint64_t since = mb_clock();
+            if (blockIdx.x == 0) {
+                for (;;) {
+                    if (__hip_atomic_load(&h->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= cur) {
+                        g = static_cast<uint64_t>(cur) << 1;
+                        break;
+                    }
+                    if (__hip_atomic_load(&h->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                        mb_clock() - since > timeout) {
+                        g = (static_cast<uint64_t>(cur - 1) << 1) | 1u;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                __hip_atomic_store(&d->go, g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                for (;;) {
+                    g = __hip_atomic_load(&d->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((g >> 1) >= cur || (g & 1u)) break;
+                    if (mb_clock() - since > 2 * timeout) {  // block 0 is not running: leave
+                        g = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            go_s = g;
+        }
+        __syncthreads();
+        if ((go_s >> 1) < cur) break;  // leaving: job cur never handed out
+        // Job cur's arguments and inputs are in host memory the host wrote
+        // before posting it: nothing cached from earlier may be used.
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(&h->jobs[cur - 1]);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&job);
+            for (uint32_t i = threadIdx.x; i < sizeof(MailboxJob) / 4; i += BT)
+                dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        const uint32_t nblk = job.blocks;
+        for (uint32_t lb = blockIdx.x; lb < nblk; lb += gridDim.x) {
+            matmul_block<K, MG, BT, true>(job.a, lb, nblk, lds4);
+            __syncthreads();  // the next logical block rebuilds the LDS tables
+        }
+        // This wave's outputs reach host memory before the block reports.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t prev = __hip_atomic_fetch_add(&d->arrive[cur - 1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev + 1 == gridDim.x)
+                __hip_atomic_store(&h->done[cur - 1], static_cast<uint64_t>(cur), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    // The last block out zeroes the device words for the next launch on
+    // this stream (kernel boundaries order the two).
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&d->left, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x) {
+        __hip_atomic_store(&d->go, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < kMailboxJobs; ++j)
+            __hip_atomic_store(&d->arrive[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&d->left, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+struct MailboxVariant {
+    int K, MG;
+    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t);
+};
+const MailboxVariant kMailbox[] = {
+    {10, 4, rs_mailbox_kernel<10, 4, 256>},  // RS(10,4): BASELINE config 1
+    {4, 4, rs_mailbox_kernel<4, 4, 256>},    // RS(4,2): the plugin default (main.go:34-35)
+};
+const MailboxVariant* mailbox_variant(int k, int rows) {
+    for (const MailboxVariant& v : kMailbox)
+        if (v.K == k && rows >= 1 && rows <= v.MG) return &v;
+    return nullptr;
+}
+
 __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint8_t* p, size_t len,
                                                                uint64_t seed) {
     const size_t nq = len / 8;
@@ -425,6 +534,28 @@ const Variant& pick(int k, int rows) {
 }  // namespace
 
 const char* variant_name(int k, int rows) { return pick(k, rows).name; }
+
+bool mailbox_supported(int k, int rows) { return mailbox_variant(k, rows) != nullptr; }
+
+void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job) {
+    const MailboxVariant* v = mailbox_variant(static_cast<int>(a.k), max_e);
+    const int mg = v ? v->MG : 4;
+    job->a = a;
+    job->a.iters = 1;
+    job->a.chunks = (a.ncols16 + kBlock - 1) / kBlock;
+    job->a.groups = static_cast<uint32_t>((max_e + mg - 1) / mg);
+    job->a.xcd = 0;  // the logical blocks are dealt over the grid's blocks anyway
+    job->blocks = static_cast<uint32_t>(a.stripes * job->a.chunks * job->a.groups);
+}
+
+hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t grid, uint64_t timeout,
+                          hipStream_t stream) {
+    const MailboxVariant* v = mailbox_variant(k, rows);
+    if (!v || grid == 0 || njobs < 1 || njobs > kMailboxJobs) return hipErrorInvalidValue;
+    const size_t lds = static_cast<size_t>(k) * ((v->MG + 3) / 4) * kStepWords * 4 + k * sizeof(void*);
+    hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), lds, stream, h, d, static_cast<uint32_t>(njobs), timeout);
+    return hipGetLastError();
+}
 
 hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream) {
     if (a.stripes == 0 || a.ncols16 == 0 || max_e <= 0) return hipSuccess;

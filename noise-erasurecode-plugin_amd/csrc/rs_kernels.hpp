@@ -56,6 +56,48 @@ struct MatArgs {
 // variant for (k, m).  max_e bounds cnt[] over all patterns.
 hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream);
 
+// Mailbox grid (rs_encode / rs_decode of one small message): one launch per
+// call of the split-table kernel that then takes the call's column-chunk
+// jobs from pinned host memory as the host stages them -- instead of a
+// launch, a dispatch and a completion event per chunk.  The host writes job
+// j (1-based) into jobs[j - 1], then posted = j; the grid codes it and
+// writes done[j - 1] = j.  quit (host) ends the grid after the jobs it
+// already handed out.
+constexpr int kMailboxJobs = 4;
+struct MailboxJob {
+    MatArgs a;        // chunks / groups / iters planned (plan_mailbox_job), xcd 0
+    uint32_t blocks;  // logical blocks of the job
+    uint32_t pad[3];
+};
+struct MailboxHost {  // pinned (coherent), device-mapped; read by the grid with system-scope loads
+    uint64_t posted;  // host: jobs posted so far
+    uint64_t quit;    // host: nonzero = leave after the jobs handed out
+    uint64_t pad0[14];
+    uint64_t done[kMailboxJobs];  // grid: done[j - 1] = j once job j is coded
+    uint64_t pad1[12];
+    MailboxJob jobs[kMailboxJobs];
+};
+struct MailboxDev {  // device memory: zero between launches (the grid's last block out zeroes it)
+    uint64_t go;      // jobs handed out << 1 | leaving
+    uint32_t left;    // blocks that have left
+    uint32_t arrive[kMailboxJobs];  // blocks finished with job j
+    uint32_t pad[9];
+};
+
+// Whether a mailbox grid serves jobs of k survivors and up to `rows`
+// outputs per stripe (the split-table variants for RS(10,4) and RS(4,2)).
+bool mailbox_supported(int k, int rows);
+// Fills job->a's launch plan (as launch_matmul would) and job->blocks.
+void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job);
+// Launches a grid of `grid` blocks for `njobs` (1..kMailboxJobs) jobs.  Its
+// block 0 waits at most `timeout` device wall-clock ticks
+// (hipDeviceAttributeWallClockRate) for a job to be posted, the others
+// twice that for block 0; a grid that gives up leaves its remaining jobs
+// undone (the caller codes them with ordinary launches after the stream
+// drained).  h is the device alias of the MailboxHost.
+hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t grid, uint64_t timeout,
+                          hipStream_t stream);
+
 // Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
 const char* variant_name(int k, int rows);  // kernel coding up to `rows` outputs per stripe
 

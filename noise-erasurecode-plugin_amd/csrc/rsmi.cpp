@@ -222,6 +222,13 @@ struct Lease {
     Staging st_onepat;                 // host-API decode: the one-pattern table, read in place by the kernel
     Staging st_out;                    // decode_in_place: regenerated shares when dst is not engine-pinned
     Staging st_in;                     // decode_staged / encode_staged: a small message's survivors
+    // Mailbox grid of a staged single message (MailboxCall): the job board
+    // in pinned coherent memory, its device alias and the grid's device
+    // words; allocated on first use.
+    rsmi::MailboxHost* mb = nullptr;
+    rsmi::MailboxHost* mb_dev = nullptr;
+    rsmi::MailboxDev* mbd = nullptr;
+    uint64_t mb_timeout = 0;  // the grid's wait for a post in device wall-clock ticks (mailbox_timeout_us)
     DevBuf d_stripe_pat, d_batch, d_pack, d_pieces, d_onepat;
     std::unique_ptr<rsmi::HostPipeline> pipe;  // host-buffer API, created on first use
     std::vector<uint32_t> pid, start;          // reconstruct scratch
@@ -278,6 +285,8 @@ struct Lease {
         st_out.destroy();
         st_in.destroy();
         for (DevBuf* b : {&d_stripe_pat, &d_batch, &d_pack, &d_pieces, &d_onepat}) b->release();
+        if (mb) (void)hipHostFree(mb);
+        if (mbd) (void)hipFree(mbd);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         if (dev_done) (void)hipEventDestroy(dev_done);
@@ -339,6 +348,7 @@ struct rs_ctx {
     std::atomic<int64_t> decodes_in_place{0};                     // rs_decode from engine-pinned memory
     std::atomic<int64_t> rec_stripes_table{0}, rec_stripes_syndrome{0};  // launch_reconstruct's kernels (rs_stat)
     std::atomic<int64_t> encode_batches{0};                              // rs_encode_batch calls through the GPU
+    std::atomic<int64_t> mailbox_calls{0}, mailbox_recovered{0};         // MailboxCall (rs_stat)
     hipEvent_t pat_ev = nullptr;
     hipStream_t build_stream = nullptr;  // pattern builds (flush_patterns), off every caller's stream
     hipEvent_t caller_ev = nullptr;      // the building caller's stream tail (build_after_caller)
@@ -1210,6 +1220,142 @@ void join_chunks(Lease& L, int launched) {
         }
 }
 
+// Mailbox grid for one staged message (rs_kernels.hpp MailboxHost): one
+// launch before the first chunk is staged, then each chunk is a job posted
+// through pinned memory and its completion a word the host polls -- the
+// per-chunk launch (4.3 us), dispatch (5 us), gap between the chunks'
+// kernels (5.4 us) and completion event of profiles/r06h/ go.  Off with
+// RSMI_MAILBOX=0; only for the split-table variants that have a mailbox
+// twin (RS(10,4), RS(4,2)) and for calls of at least two chunks.
+bool mailbox_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSMI_MAILBOX");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+// How long the grid's block 0 waits for a post (RSMI_MAILBOX_TIMEOUT_US,
+// default 20 ms; tests shorten it to make grids give up); a waiting caller
+// gives the grid 2.5x that (at least 1 ms) before it drains the stream and
+// launches the undone chunks itself.
+long mailbox_timeout_us() {
+    static const long us = [] {
+        const char* e = std::getenv("RSMI_MAILBOX_TIMEOUT_US");
+        const long v = e ? std::atol(e) : 20000;
+        return v > 0 ? v : 20000;
+    }();
+    return us;
+}
+
+class MailboxCall {
+public:
+    // Launches the grid for njobs jobs of up to `rows` outputs per stripe
+    // and `blocks` logical blocks each on L.stream (after L.begin), or
+    // leaves ok() false: the caller launches its chunks itself.
+    MailboxCall(rs_ctx* c, Lease& L, int njobs, int rows, uint32_t blocks) : c_(c), L_(L), njobs_(njobs) {
+        if (!mailbox_on() || njobs < 2 || njobs > rsmi::kMailboxJobs || !rsmi::mailbox_supported(c->k, rows)) return;
+        if (!L.mb) {
+            void* h = nullptr;
+            if (hipHostMalloc(&h, sizeof(rsmi::MailboxHost), hipHostMallocCoherent) != hipSuccess) return;
+            void* hd = nullptr;
+            void* dd = nullptr;
+            if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess || hipMalloc(&dd, sizeof(rsmi::MailboxDev)) != hipSuccess ||
+                hipMemset(dd, 0, sizeof(rsmi::MailboxDev)) != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipHostFree(h);
+                if (dd) (void)hipFree(dd);
+                return;
+            }
+            int khz = 0;
+            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0)
+                khz = 100000;
+            std::memset(h, 0, sizeof(rsmi::MailboxHost));
+            L.mb = static_cast<rsmi::MailboxHost*>(h);
+            L.mb_dev = static_cast<rsmi::MailboxHost*>(hd);
+            L.mbd = static_cast<rsmi::MailboxDev*>(dd);
+            L.mb_timeout = static_cast<uint64_t>(khz) * mailbox_timeout_us() / 1000;
+        }
+        // The previous call's grid reads the board no more (its jobs were
+        // all waited for, or it was drained): reset it for this one.
+        rsmi::MailboxHost* h = L.mb;
+        __atomic_store_n(&h->quit, uint64_t(0), __ATOMIC_RELAXED);
+        for (uint64_t& d : h->done) __atomic_store_n(&d, uint64_t(0), __ATOMIC_RELAXED);
+        __atomic_store_n(&h->posted, uint64_t(0), __ATOMIC_RELEASE);
+        const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 256));
+        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, njobs, c->k, rows, grid, L.mb_timeout, L.stream) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        ok_ = true;
+        ++c->mailbox_calls;
+    }
+    ~MailboxCall() {
+        if (!ok_) return;
+        if (waited_ < njobs_) {  // an early return: the grid leaves once it sees quit, then the stream drains
+            __atomic_store_n(&L_.mb->quit, uint64_t(1), __ATOMIC_RELEASE);
+            (void)hipStreamSynchronize(L_.stream);
+        }
+    }
+    bool ok() const { return ok_; }
+    // Job j (0-based): its arguments into the board, then the post.
+    void post(int j, const rsmi::MatArgs& a, int max_e) {
+        rsmi::MailboxJob job;
+        rsmi::plan_mailbox_job(a, max_e, &job);
+        std::memcpy(&L_.mb->jobs[j], &job, sizeof(job));
+        max_e_[j] = max_e;
+        __atomic_store_n(&L_.mb->posted, static_cast<uint64_t>(j + 1), __ATOMIC_RELEASE);
+        posted_ = j + 1;
+    }
+    // Waits for job j.  A grid that gave up (mailbox_timeout_us) or could
+    // not run leaves jobs undone: after 2.5x that the caller asks it to
+    // leave, drains the stream and launches what is still undone itself.
+    hipError_t wait(int j) {
+        const uint64_t want = static_cast<uint64_t>(j + 1);
+        const uint64_t* done = &L_.mb->done[j];
+        if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != want) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (unsigned spin = 0;; ++spin) {
+                if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == want) break;
+                if ((spin & 255u) != 255u) {
+                    __builtin_ia32_pause();
+                    continue;
+                }
+                const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+                if (us > std::max(1000L, mailbox_timeout_us() * 5 / 2)) return recover(j);
+                if (us > 200) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+        }
+        waited_ = std::max(waited_, j + 1);
+        return hipSuccess;
+    }
+
+private:
+    hipError_t recover(int j) {
+        __atomic_store_n(&L_.mb->quit, uint64_t(1), __ATOMIC_RELEASE);
+        hipError_t e = hipStreamSynchronize(L_.stream);  // the grid has left
+        for (int i = 0; i < posted_ && e == hipSuccess; ++i)
+            if (__atomic_load_n(&L_.mb->done[i], __ATOMIC_ACQUIRE) != static_cast<uint64_t>(i + 1)) {
+                rsmi::MatArgs a = L_.mb->jobs[i].a;
+                e = rsmi::launch_matmul(a, max_e_[i], L_.stream);
+                if (e == hipSuccess) __atomic_store_n(&L_.mb->done[i], static_cast<uint64_t>(i + 1), __ATOMIC_RELAXED);
+            }
+        if (e == hipSuccess) e = hipStreamSynchronize(L_.stream);
+        if (!recovered_) ++c_->mailbox_recovered;
+        recovered_ = true;
+        waited_ = std::max(waited_, j + 1);
+        if (j >= posted_) return hipErrorInvalidValue;
+        return e;
+    }
+
+    rs_ctx* c_;
+    Lease& L_;
+    int njobs_;
+    bool ok_ = false, recovered_ = false;
+    int posted_ = 0, waited_ = 0;
+    int max_e_[rsmi::kMailboxJobs] = {};
+};
+
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
 // Rebuild's choice `surv` is read at device address dev[j] (column chunk by
 // column chunk when nch > 1, the copies `stage` lists filling each chunk's
@@ -1226,7 +1372,20 @@ using StageFn = std::function<std::vector<rsmi::CopyPool::Piece>(size_t off, siz
 constexpr int kDecodeNoStaging = -1000;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
-                  bool present_done, int nch = 1, const StageFn& stage = nullptr);
+                  bool present_done, int nch = 1, const StageFn& stage = nullptr,
+                  const std::vector<uint8_t>* staged_to_dst = nullptr);
+
+// RSMI_FUSED_PRESENT=1: decode_staged's staging copy of a present data share
+// also writes its row of dst (stage_copy2), so the share is read once, not
+// once for the staging and again for the present-share copy.
+bool fused_present() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSMI_FUSED_PRESENT");
+        const char* a = std::getenv("RSMI_ASYNC_COPIES");  // the pool's copies know one destination only
+        return e && std::atoi(e) != 0 && !(a && std::atoi(a) != 0);
+    }();
+    return on;
+}
 
 // Column chunks of a staged small message: chunk c covers bytes
 // [off(c), off(c + 1)) of every shard, offsets multiples of 16.  Two chunks
@@ -1292,14 +1451,24 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     std::vector<uint64_t> dev(k);
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
     for (int j = 0; j < k; ++j) dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
-    // survivors' columns [off, off + w) into staging (non-temporal), chunk by chunk
+    // survivors' columns [off, off + w) into staging (non-temporal), chunk by
+    // chunk; with fused_present() a present data share's columns go to its
+    // row of dst in the same pass
+    std::vector<uint8_t> to_dst(static_cast<size_t>(k), 0);
+    if (fused_present())
+        for (int j = 0; j < k; ++j)
+            if (surv[j] < k && dst + static_cast<size_t>(surv[j]) * S != by_id[surv[j]]) to_dst[surv[j]] = 1;
     auto stage = [&](size_t off, size_t w) {
         std::vector<rsmi::CopyPool::Piece> v;
-        for (int j = 0; j < k; ++j) v.push_back({st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w, true});
+        for (int j = 0; j < k; ++j) {
+            rsmi::CopyPool::Piece q{st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w, true};
+            if (surv[j] < k && to_dst[surv[j]]) q.dst2 = dst + static_cast<size_t>(surv[j]) * S + off;
+            v.push_back(q);
+        }
         return v;
     };
     const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
-                                stage_chunks(static_cast<size_t>(k) * S), stage);
+                                stage_chunks(static_cast<size_t>(k) * S), stage, &to_dst);
     if (r == kDecodeNoStaging) return false;
     *rc = r;
     return true;
@@ -1307,7 +1476,7 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
 
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
-                  bool present_done, int nch, const StageFn& stage) {
+                  bool present_done, int nch, const StageFn& stage, const std::vector<uint8_t>* staged_to_dst) {
     const int k = c->k;
     const size_t span = round_up(S, 16);
     std::vector<int> missing;
@@ -1318,7 +1487,8 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
         std::vector<rsmi::CopyPool::Piece> v;
         if (!present_done)
             for (int i = 0; i < k; ++i)
-                if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i]) v.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
+                if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i] && !(staged_to_dst && (*staged_to_dst)[i]))
+                    v.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
         return v;
     };
     if (e == 0) {
@@ -1385,8 +1555,16 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     }
     L.begin(s);
     if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
+    // A staged message's chunks go to a mailbox grid launched now, whose
+    // dispatch overlaps the staging of chunk 0 (MailboxCall).
+    uint32_t mb_blocks = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+        const size_t w = chunk_off(S, ch + 1, nch) - chunk_off(S, ch, nch);
+        mb_blocks = std::max<uint32_t>(mb_blocks, static_cast<uint32_t>((round_up(w, 16) / 16 + 255) / 256 * ((e + 3) / 4)));
+    }
+    MailboxCall mb(c, L, stage && !async_copies && L.chunk_stream(1) == s ? nch : 0, e, mb_blocks);
     // every chunk records its event unless RSMI_CHUNK_EVENTS=0 on one stream
-    const bool ev_each = chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
+    const bool ev_each = mb.ok() || chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t err = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && err == hipSuccess; ++ch) {
@@ -1398,7 +1576,10 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                 staged[ch] = nullptr;
             } else {
                 const std::vector<rsmi::CopyPool::Piece> v = stage(off, w);
-                for (const rsmi::CopyPool::Piece& q : v) rsmi::stage_copy(q.dst, q.src, q.len);
+                for (const rsmi::CopyPool::Piece& q : v) {
+                    if (q.dst2) rsmi::stage_copy2(q.dst, q.dst2, q.src, q.len);
+                    else rsmi::stage_copy(q.dst, q.src, q.len);
+                }
                 rsmi::stage_fence();
             }
         }
@@ -1417,8 +1598,12 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                                         : oalias + static_cast<uint64_t>(t) * span + off;
             a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
         }
-        err = rsmi::launch_matmul(a, e, cs);
-        if (err == hipSuccess && (ev_each || ch == nch - 1)) err = hipEventRecord(L.ev[ch], cs);
+        if (mb.ok()) {
+            mb.post(ch, a, e);
+        } else {
+            err = rsmi::launch_matmul(a, e, cs);
+            if (err == hipSuccess && (ev_each || ch == nch - 1)) err = hipEventRecord(L.ev[ch], cs);
+        }
         if (err == hipSuccess) ++launched;
         rsmi::trace_mark(ch ? "launch1" : "launch0");
     }
@@ -1430,7 +1615,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     rsmi::trace_mark("copy_present");
     for (int ch = 0; ch < launched; ++ch) {
         if (!ev_each && ch < nch - 1) continue;  // no event of its own: copied out with the last chunk
-        const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
+        const hipError_t w8 = mb.ok() ? mb.wait(ch) : rsmi::wait_event(L.ev[ch]);
         rsmi::trace_mark(ch ? "wait1" : "wait0");
         if (err == hipSuccess) err = w8;
         if (err != hipSuccess || dst_direct) continue;
@@ -1477,7 +1662,14 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
         for (int ch = 1; ch < nch; ++ch) staged[ch] = pool.start(pieces(ch), size_t(128) << 10);
     L.begin(s);
     if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
-    const bool ev_each = chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
+    uint32_t mb_blocks = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+        const size_t w = chunk_off(S, ch + 1, nch) - chunk_off(S, ch, nch);
+        mb_blocks = std::max<uint32_t>(mb_blocks, static_cast<uint32_t>((round_up(w, 16) / 16 + 255) / 256 * ((m + 3) / 4)));
+    }
+    MailboxCall mb(c, L, !c->bitslice && !async_copies && L.chunk_stream(1) == s ? nch : 0, static_cast<int>(m),
+                   mb_blocks);
+    const bool ev_each = mb.ok() || chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t e = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && e == hipSuccess; ++ch) {
@@ -1494,8 +1686,12 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
         rsmi::MatArgs a = base_args(c, static_cast<uint8_t*>(din) + off, 0, static_cast<uint8_t*>(dout) + off, 0, span, w, 1);
         set_patterns(c, 1, c->d_encpat.p, a);
         a.stripe_desc = nullptr;
-        e = launch_encode(c, a, cs);
-        if (e == hipSuccess && (ev_each || ch == nch - 1)) e = hipEventRecord(L.ev[ch], cs);
+        if (mb.ok()) {
+            mb.post(ch, a, static_cast<int>(m));
+        } else {
+            e = launch_encode(c, a, cs);
+            if (e == hipSuccess && (ev_each || ch == nch - 1)) e = hipEventRecord(L.ev[ch], cs);
+        }
         if (e == hipSuccess) ++launched;
         rsmi::trace_mark(ch ? "launch1" : "launch0");
     }
@@ -1504,7 +1700,7 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
     for (rsmi::CopyPool::Async* j : staged) pool.finish(j);  // a failed launch left some unjoined
     for (int ch = 0; ch < launched; ++ch) {
         if (!ev_each && ch < nch - 1) continue;  // copied out with the last chunk
-        const hipError_t w8 = rsmi::wait_event(L.ev[ch]);
+        const hipError_t w8 = mb.ok() ? mb.wait(ch) : rsmi::wait_event(L.ev[ch]);
         rsmi::trace_mark(ch ? "wait1" : "wait0");
         if (e == hipSuccess) e = w8;
         if (e != hipSuccess) continue;
@@ -2027,6 +2223,8 @@ int64_t rs_stat(const rs_ctx* c, int which) {
         case RS_STAT_REC_STRIPES_TABLE: return c->rec_stripes_table.load();
         case RS_STAT_REC_STRIPES_SYNDROME: return c->rec_stripes_syndrome.load();
         case RS_STAT_ENCODE_BATCHES: return c->encode_batches.load();
+        case RS_STAT_MAILBOX_CALLS: return c->mailbox_calls.load();
+        case RS_STAT_MAILBOX_RECOVERED: return c->mailbox_recovered.load();
         case RS_STAT_LEASES: {
             std::lock_guard<std::mutex> lk(const_cast<rs_ctx*>(c)->lease_mu);
             return static_cast<int64_t>(c->leases.size());

@@ -410,7 +410,7 @@ class FEC:
 
     (STAT_PATTERNS, STAT_EVICTIONS, STAT_BATCHES_IN_PLACE, STAT_BATCHES_STAGED, STAT_LEASES,
      STAT_ENCODES_IN_PLACE, STAT_DECODES_IN_PLACE, STAT_REC_STRIPES_TABLE, STAT_REC_STRIPES_SYNDROME,
-     STAT_ENCODE_BATCHES) = range(10)
+     STAT_ENCODE_BATCHES, STAT_MAILBOX_CALLS, STAT_MAILBOX_RECOVERED) = range(12)
 
     def stat(self, which: int) -> int:
         return _lib().rs_stat(self._h, which)

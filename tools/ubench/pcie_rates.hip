@@ -77,6 +77,13 @@ int main() {
         ms = med_ms([&] { hipLaunchKernelGGL(read_host, dim3(blocks), dim3(256), 0, s1, (const uint4*)d2, (uint4*)hd2, N / 16); }, s1);
         std::printf("kernel writes pinned host 16 MiB (%d blocks): %.1f GB/s\n", blocks, gbs(ms, N));
     }
+    // A single config-1 chunk's sizes: one kernel reading 256 KiB .. 1 MiB of
+    // pinned host memory (one 16-byte column per lane, as rs_matmul_kernel).
+    for (size_t bytes : {size_t(256) << 10, size_t(512) << 10, size_t(1) << 20}) {
+        const int blocks = static_cast<int>(bytes / 16 / 256);
+        ms = med_ms([&] { hipLaunchKernelGGL(read_host, dim3(blocks), dim3(256), 0, s1, (const uint4*)hd1, (uint4*)d1, bytes / 16); }, s1);
+        std::printf("kernel reads %zu KiB of pinned host (%d blocks): %.2f us, %.1f GB/s\n", bytes >> 10, blocks, ms * 1e3, gbs(ms, bytes));
+    }
     ms = med_ms([&] {
         hipLaunchKernelGGL(read_host, dim3(1024), dim3(256), 0, s2, (const uint4*)d2, (uint4*)hd2, N / 16 * 4 / 10);
         (void)hipEventRecord(e2, s2);
