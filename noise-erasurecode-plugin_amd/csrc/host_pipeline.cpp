@@ -86,48 +86,6 @@ void stage_copy(void* dst, const void* src, size_t n) {
     std::memcpy(dst, src, n);
 }
 
-void stage_copy2(void* staging, void* dst, const void* src, size_t n) {
-#if defined(__x86_64__)
-    if (stage_nt() && n >= 4096) {
-        uint8_t* d = static_cast<uint8_t*>(staging);
-        uint8_t* o = static_cast<uint8_t*>(dst);
-        const uint8_t* s = static_cast<const uint8_t*>(src);
-        const size_t head = (16u - (reinterpret_cast<uintptr_t>(d) & 15u)) & 15u;
-        std::memcpy(d, s, head);
-        std::memcpy(o, s, head);
-        d += head;
-        o += head;
-        s += head;
-        n -= head;
-        size_t i = 0;
-        for (; i + 64 <= n; i += 64) {
-            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
-            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 16));
-            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 32));
-            const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 48));
-            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16), b);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 32), c);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 48), e);
-            _mm_storeu_si128(reinterpret_cast<__m128i*>(o + i), a);
-            _mm_storeu_si128(reinterpret_cast<__m128i*>(o + i + 16), b);
-            _mm_storeu_si128(reinterpret_cast<__m128i*>(o + i + 32), c);
-            _mm_storeu_si128(reinterpret_cast<__m128i*>(o + i + 48), e);
-        }
-        for (; i + 16 <= n; i += 16) {
-            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
-            _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
-            _mm_storeu_si128(reinterpret_cast<__m128i*>(o + i), a);
-        }
-        std::memcpy(d + i, s + i, n - i);
-        std::memcpy(o + i, s + i, n - i);
-        return;
-    }
-#endif
-    std::memcpy(staging, src, n);
-    std::memcpy(dst, src, n);
-}
-
 namespace {
 bool trace_on() {
     static const bool on = [] {

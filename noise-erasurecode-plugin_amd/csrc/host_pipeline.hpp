@@ -39,7 +39,6 @@ public:
         const void* src;
         size_t len;
         bool nt = false;  // dst is pinned staging a kernel reads next: stage_copy (+ fence)
-        void* dst2 = nullptr;  // nt pieces copied inline only: a second destination (stage_copy2)
     };
     // Copies every piece (split further into <= 1 MiB parts); returns when done.
     void run(const std::vector<Piece>& pieces);
@@ -100,11 +99,6 @@ hipError_t wait_event(hipEvent_t ev);
 // snoop them out: one config-1 message's kernel reads its 1 MiB 4.7 us faster
 // (tools/stream_probe.hip, profiles/r05j/).  RSMI_STAGE_NT=0: plain memcpy.
 void stage_copy(void* dst, const void* src, size_t n);
-// stage_copy into `staging` that also leaves the bytes in `dst` (ordinary
-// stores): one read of src for a present data share that is both a
-// survivor the kernel reads and a row of the caller's output
-// (RSMI_FUSED_PRESENT, rsmi.cpp decode_staged).
-void stage_copy2(void* staging, void* dst, const void* src, size_t n);
 
 // Phase trace of the single-message host calls (RSMI_TRACE=1, diagnostics
 // only; one branch on a static flag otherwise): trace_begin() at a call's

@@ -357,96 +357,78 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
 }
 
 // ------------------------------------------------------------- mailbox --
-// One grid per single-message call (rs_kernels.hpp MailboxHost): block 0
-// polls `posted` over PCIe and hands each job to the grid through
-// MailboxDev::go; every block codes its share of the job's logical blocks
-// and the last one to finish writes done[j - 1].  A call's chunks then cost
-// the host a 0.3 KiB write each instead of a launch and an event, and the
-// grid's dispatch overlaps the staging of the first chunk (profiles/r06h/:
-// 4.3 us to launch a chunk, 5 us to dispatch it, 5.4 us between two
-// chunks' kernels).  Every wave leaves: after the last job, on quit, or on
-// a timeout.
+// One grid per single-message call (rs_kernels.hpp MailboxHost), a group of
+// `per_job` blocks per job: the group's blocks poll `posted` over PCIe and
+// code their job as soon as it is posted -- while the groups of earlier jobs
+// are still reading theirs, so the PCIe reads of consecutive chunks overlap
+// instead of each chunk paying the read latency ramp again (a kernel reading
+// 256 KiB / 512 KiB / 1 MiB of pinned host memory takes 11 / 17 / 30 us,
+// profiles/r06n/pcie_rates.txt).  The last block of a group to finish
+// writes done[j - 1].  The call's chunks then cost the host a 0.3 KiB write
+// each instead of a launch and an event, and the grid's dispatch overlaps the
+// staging of the first chunk (profiles/r06h/: 4.3 us to launch a chunk,
+// 5 us to dispatch it, 5.4 us between two chunks' kernels).  Every wave
+// leaves: after its job, on quit, or when its job is not posted in time.
 __device__ __forceinline__ uint64_t mb_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
 template <int K, int MG, int BT>
-__global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxDev* d, uint32_t njobs,
+__global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxDev* d, uint32_t per_job,
                                                         uint64_t timeout) {
     extern __shared__ uint4 lds4[];
     __shared__ MailboxJob job;
-    __shared__ uint64_t go_s;
-    for (uint32_t cur = 1; cur <= njobs; ++cur) {
-        if (threadIdx.x == 0) {
-            uint64_t g;
-            const uint64_t since = mb_clock();
-            if (blockIdx.x == 0) {
-                for (;;) {
-                    if (__hip_atomic_load(&h->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= cur) {
-                        g = static_cast<uint64_t>(cur) << 1;
-                        break;
-                    }
-                    if (__hip_atomic_load(&h->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                        mb_clock() - since > timeout) {
-                        g = (static_cast<uint64_t>(cur - 1) << 1) | 1u;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                __hip_atomic_store(&d->go, g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                for (;;) {
-                    g = __hip_atomic_load(&d->go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((g >> 1) >= cur || (g & 1u)) break;
-                    if (mb_clock() - since > 2 * timeout) {  // block 0 is not running: leave
-                        g = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
+    __shared__ uint32_t go_s;
+    const uint32_t j = blockIdx.x / per_job;  // this block's job, 0-based
+    if (threadIdx.x == 0) {
+        uint32_t go = 0;
+        const uint64_t since = mb_clock();
+        for (;;) {
+            if (__hip_atomic_load(&h->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) > j) {
+                go = 1;
+                break;
             }
-            go_s = g;
+            if (__hip_atomic_load(&h->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) || mb_clock() - since > timeout)
+                break;
+            __builtin_amdgcn_s_sleep(4);
         }
-        __syncthreads();
-        if ((go_s >> 1) < cur) break;  // leaving: job cur never handed out
-        // Job cur's arguments and inputs are in host memory the host wrote
+        go_s = go;
+    }
+    __syncthreads();
+    if (go_s) {
+        // Job j's arguments and inputs are in host memory the host wrote
         // before posting it: nothing cached from earlier may be used.
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(&h->jobs[cur - 1]);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(&h->jobs[j]);
             uint32_t* dst = reinterpret_cast<uint32_t*>(&job);
             for (uint32_t i = threadIdx.x; i < sizeof(MailboxJob) / 4; i += BT)
                 dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
         const uint32_t nblk = job.blocks;
-        for (uint32_t lb = blockIdx.x; lb < nblk; lb += gridDim.x) {
+        for (uint32_t lb = blockIdx.x - j * per_job; lb < nblk; lb += per_job) {
             matmul_block<K, MG, BT, true>(job.a, lb, nblk, lds4);
             __syncthreads();  // the next logical block rebuilds the LDS tables
         }
         // This wave's outputs reach host memory before the block reports.
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t prev = __hip_atomic_fetch_add(&d->arrive[cur - 1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev + 1 == gridDim.x)
-                __hip_atomic_store(&h->done[cur - 1], static_cast<uint64_t>(cur), __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (threadIdx.x == 0 &&
+            __hip_atomic_fetch_add(&d->arrive[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == per_job)
+            __hip_atomic_store(&h->done[j], static_cast<uint64_t>(j + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // The last block out zeroes the device words for the next launch on
+    // The last block out zeroes the device counters for the next launch on
     // this stream (kernel boundaries order the two).
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(&d->left, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x) {
-        __hip_atomic_store(&d->go, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int j = 0; j < kMailboxJobs; ++j)
-            __hip_atomic_store(&d->arrive[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < kMailboxJobs; ++i)
+            __hip_atomic_store(&d->arrive[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&d->left, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 struct MailboxVariant {
     int K, MG;
-    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t);
+    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t);  // (h, d, per_job, timeout)
 };
 const MailboxVariant kMailbox[] = {
     {10, 4, rs_mailbox_kernel<10, 4, 256>},  // RS(10,4): BASELINE config 1
@@ -548,12 +530,13 @@ void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job) {
     job->blocks = static_cast<uint32_t>(a.stripes * job->a.chunks * job->a.groups);
 }
 
-hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t grid, uint64_t timeout,
-                          hipStream_t stream) {
+hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t per_job,
+                          uint64_t timeout, hipStream_t stream) {
     const MailboxVariant* v = mailbox_variant(k, rows);
-    if (!v || grid == 0 || njobs < 1 || njobs > kMailboxJobs) return hipErrorInvalidValue;
+    if (!v || per_job == 0 || njobs < 1 || njobs > kMailboxJobs) return hipErrorInvalidValue;
     const size_t lds = static_cast<size_t>(k) * ((v->MG + 3) / 4) * kStepWords * 4 + k * sizeof(void*);
-    hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), lds, stream, h, d, static_cast<uint32_t>(njobs), timeout);
+    hipLaunchKernelGGL(v->fn, dim3(per_job * static_cast<uint32_t>(njobs)), dim3(kBlock), lds, stream, h, d, per_job,
+                       timeout);
     return hipGetLastError();
 }
 

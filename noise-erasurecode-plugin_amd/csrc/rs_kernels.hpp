@@ -57,12 +57,12 @@ struct MatArgs {
 hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream);
 
 // Mailbox grid (rs_encode / rs_decode of one small message): one launch per
-// call of the split-table kernel that then takes the call's column-chunk
-// jobs from pinned host memory as the host stages them -- instead of a
-// launch, a dispatch and a completion event per chunk.  The host writes job
-// j (1-based) into jobs[j - 1], then posted = j; the grid codes it and
-// writes done[j - 1] = j.  quit (host) ends the grid after the jobs it
-// already handed out.
+// call of the split-table kernel, a group of blocks per column-chunk job,
+// each group coding its job as soon as the host has staged and posted it --
+// instead of a launch, a dispatch and a completion event per chunk.  The
+// host writes job j (1-based) into jobs[j - 1], then posted = j; job j's
+// group codes it and writes done[j - 1] = j.  quit (host) makes the groups
+// still waiting for their job leave.
 constexpr int kMailboxJobs = 4;
 struct MailboxJob {
     MatArgs a;        // chunks / groups / iters planned (plan_mailbox_job), xcd 0
@@ -71,17 +71,16 @@ struct MailboxJob {
 };
 struct MailboxHost {  // pinned (coherent), device-mapped; read by the grid with system-scope loads
     uint64_t posted;  // host: jobs posted so far
-    uint64_t quit;    // host: nonzero = leave after the jobs handed out
+    uint64_t quit;    // host: nonzero = groups still waiting leave
     uint64_t pad0[14];
     uint64_t done[kMailboxJobs];  // grid: done[j - 1] = j once job j is coded
     uint64_t pad1[12];
     MailboxJob jobs[kMailboxJobs];
 };
 struct MailboxDev {  // device memory: zero between launches (the grid's last block out zeroes it)
-    uint64_t go;      // jobs handed out << 1 | leaving
     uint32_t left;    // blocks that have left
-    uint32_t arrive[kMailboxJobs];  // blocks finished with job j
-    uint32_t pad[9];
+    uint32_t arrive[kMailboxJobs];  // blocks of job j's group finished with it
+    uint32_t pad[11];
 };
 
 // Whether a mailbox grid serves jobs of k survivors and up to `rows`
@@ -89,14 +88,14 @@ struct MailboxDev {  // device memory: zero between launches (the grid's last bl
 bool mailbox_supported(int k, int rows);
 // Fills job->a's launch plan (as launch_matmul would) and job->blocks.
 void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job);
-// Launches a grid of `grid` blocks for `njobs` (1..kMailboxJobs) jobs.  Its
-// block 0 waits at most `timeout` device wall-clock ticks
-// (hipDeviceAttributeWallClockRate) for a job to be posted, the others
-// twice that for block 0; a grid that gives up leaves its remaining jobs
-// undone (the caller codes them with ordinary launches after the stream
-// drained).  h is the device alias of the MailboxHost.
-hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t grid, uint64_t timeout,
-                          hipStream_t stream);
+// Launches njobs (1..kMailboxJobs) groups of per_job blocks (a group codes
+// its job's logical blocks in turn).  A block waits at most `timeout` device
+// wall-clock ticks (hipDeviceAttributeWallClockRate) for its job to be
+// posted; a job whose group gave up stays undone (the caller codes it with
+// an ordinary launch after the stream drained).  h is the device alias of
+// the MailboxHost.
+hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t per_job,
+                          uint64_t timeout, hipStream_t stream);
 
 // Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
 const char* variant_name(int k, int rows);  // kernel coding up to `rows` outputs per stripe

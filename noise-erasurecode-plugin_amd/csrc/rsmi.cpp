@@ -1282,8 +1282,8 @@ public:
         __atomic_store_n(&h->quit, uint64_t(0), __ATOMIC_RELAXED);
         for (uint64_t& d : h->done) __atomic_store_n(&d, uint64_t(0), __ATOMIC_RELAXED);
         __atomic_store_n(&h->posted, uint64_t(0), __ATOMIC_RELEASE);
-        const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 256));
-        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, njobs, c->k, rows, grid, L.mb_timeout, L.stream) != hipSuccess) {
+        const uint32_t per_job = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 64));
+        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, njobs, c->k, rows, per_job, L.mb_timeout, L.stream) != hipSuccess) {
             (void)hipGetLastError();
             return;
         }
@@ -1372,20 +1372,8 @@ using StageFn = std::function<std::vector<rsmi::CopyPool::Piece>(size_t off, siz
 constexpr int kDecodeNoStaging = -1000;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
-                  bool present_done, int nch = 1, const StageFn& stage = nullptr,
-                  const std::vector<uint8_t>* staged_to_dst = nullptr);
+                  bool present_done, int nch = 1, const StageFn& stage = nullptr);
 
-// RSMI_FUSED_PRESENT=1: decode_staged's staging copy of a present data share
-// also writes its row of dst (stage_copy2), so the share is read once, not
-// once for the staging and again for the present-share copy.
-bool fused_present() {
-    static const bool on = [] {
-        const char* e = std::getenv("RSMI_FUSED_PRESENT");
-        const char* a = std::getenv("RSMI_ASYNC_COPIES");  // the pool's copies know one destination only
-        return e && std::atoi(e) != 0 && !(a && std::atoi(a) != 0);
-    }();
-    return on;
-}
 
 // Column chunks of a staged small message: chunk c covers bytes
 // [off(c), off(c + 1)) of every shard, offsets multiples of 16.  Two chunks
@@ -1400,7 +1388,22 @@ int stage_chunks(size_t bytes) {
     if (forced) return forced;
     return bytes >= (size_t(256) << 10) ? 2 : 1;
 }
-size_t chunk_off(size_t S, int c, int nch) { return c >= nch ? S : (S * c / nch) & ~size_t(15); }
+// A two-chunk message splits at RSMI_FIRST_CHUNK_PCT percent of each shard
+// (default 50): a smaller first chunk is staged sooner, so the GPU starts
+// reading earlier while the host stages the rest.
+size_t first_chunk_pct() {
+    static const size_t pct = [] {
+        const char* e = std::getenv("RSMI_FIRST_CHUNK_PCT");
+        const long v = e ? std::atol(e) : 50;
+        return static_cast<size_t>(v >= 10 && v <= 90 ? v : 50);
+    }();
+    return pct;
+}
+size_t chunk_off(size_t S, int c, int nch) {
+    if (c >= nch) return S;
+    if (nch == 2 && c == 1) return (S * first_chunk_pct() / 100) & ~size_t(15);
+    return (S * c / nch) & ~size_t(15);
+}
 
 // rs_decode of exactly k distinct shares that all lie in engine-pinned
 // memory (pinned.hpp: an rs_arena / rs_pinned_alloc range, 16-byte aligned,
@@ -1451,24 +1454,14 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
     std::vector<uint64_t> dev(k);
     uint8_t* st = static_cast<uint8_t*>(L.st_in.p);
     for (int j = 0; j < k; ++j) dev[j] = reinterpret_cast<uint64_t>(alias) + static_cast<uint64_t>(j) * span;
-    // survivors' columns [off, off + w) into staging (non-temporal), chunk by
-    // chunk; with fused_present() a present data share's columns go to its
-    // row of dst in the same pass
-    std::vector<uint8_t> to_dst(static_cast<size_t>(k), 0);
-    if (fused_present())
-        for (int j = 0; j < k; ++j)
-            if (surv[j] < k && dst + static_cast<size_t>(surv[j]) * S != by_id[surv[j]]) to_dst[surv[j]] = 1;
+    // survivors' columns [off, off + w) into staging (non-temporal), chunk by chunk
     auto stage = [&](size_t off, size_t w) {
         std::vector<rsmi::CopyPool::Piece> v;
-        for (int j = 0; j < k; ++j) {
-            rsmi::CopyPool::Piece q{st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w, true};
-            if (surv[j] < k && to_dst[surv[j]]) q.dst2 = dst + static_cast<size_t>(surv[j]) * S + off;
-            v.push_back(q);
-        }
+        for (int j = 0; j < k; ++j) v.push_back({st + static_cast<size_t>(j) * span + off, by_id[surv[j]] + off, w, true});
         return v;
     };
     const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
-                                stage_chunks(static_cast<size_t>(k) * S), stage, &to_dst);
+                                stage_chunks(static_cast<size_t>(k) * S), stage);
     if (r == kDecodeNoStaging) return false;
     *rc = r;
     return true;
@@ -1476,7 +1469,7 @@ bool decode_staged(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, con
 
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
-                  bool present_done, int nch, const StageFn& stage, const std::vector<uint8_t>* staged_to_dst) {
+                  bool present_done, int nch, const StageFn& stage) {
     const int k = c->k;
     const size_t span = round_up(S, 16);
     std::vector<int> missing;
@@ -1487,8 +1480,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
         std::vector<rsmi::CopyPool::Piece> v;
         if (!present_done)
             for (int i = 0; i < k; ++i)
-                if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i] && !(staged_to_dst && (*staged_to_dst)[i]))
-                    v.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
+                if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i]) v.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
         return v;
     };
     if (e == 0) {
@@ -1576,10 +1568,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                 staged[ch] = nullptr;
             } else {
                 const std::vector<rsmi::CopyPool::Piece> v = stage(off, w);
-                for (const rsmi::CopyPool::Piece& q : v) {
-                    if (q.dst2) rsmi::stage_copy2(q.dst, q.dst2, q.src, q.len);
-                    else rsmi::stage_copy(q.dst, q.src, q.len);
-                }
+                for (const rsmi::CopyPool::Piece& q : v) rsmi::stage_copy(q.dst, q.src, q.len);
                 rsmi::stage_fence();
             }
         }
