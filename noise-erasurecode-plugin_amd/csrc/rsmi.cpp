@@ -1224,15 +1224,28 @@ void join_chunks(Lease& L, int launched) {
 // launch before the first chunk is staged, then each chunk is a job posted
 // through pinned memory and its completion a word the host polls -- the
 // per-chunk launch (4.3 us), dispatch (5 us), gap between the chunks'
-// kernels (5.4 us) and completion event of profiles/r06h/ go.  Off with
-// RSMI_MAILBOX=0; only for the split-table variants that have a mailbox
-// twin (RS(10,4), RS(4,2)) and for calls of at least two chunks.
+// kernels (5.4 us) and completion event of profiles/r06h/ go, and the
+// chunks' PCIe reads overlap (a block group per chunk): config-1 decode
+// 56.7-63.5 -> 47.6-48.9 us, encode 57.5-58.9 -> 50.0-50.8 us on one box
+// (profiles/r06o/).  Off with RSMI_MAILBOX=0; only for the split-table
+// variants that have a mailbox twin (RS(10,4), RS(4,2)).
 bool mailbox_on() {
     static const bool on = [] {
         const char* e = std::getenv("RSMI_MAILBOX");
         return !(e && std::atoi(e) == 0);
     }();
     return on;
+}
+// Calls of fewer chunks launch their kernel the ordinary way
+// (RSMI_MAILBOX_MIN_JOBS, default 2; 1 also gives the one-launch decode of
+// engine-pinned survivors a grid).
+int mailbox_min_jobs() {
+    static const int n = [] {
+        const char* e = std::getenv("RSMI_MAILBOX_MIN_JOBS");
+        const int v = e ? std::atoi(e) : 2;
+        return v >= 1 && v <= rsmi::kMailboxJobs ? v : 2;
+    }();
+    return n;
 }
 
 // How long the grid's block 0 waits for a post (RSMI_MAILBOX_TIMEOUT_US,
@@ -1254,7 +1267,9 @@ public:
     // and `blocks` logical blocks each on L.stream (after L.begin), or
     // leaves ok() false: the caller launches its chunks itself.
     MailboxCall(rs_ctx* c, Lease& L, int njobs, int rows, uint32_t blocks) : c_(c), L_(L), njobs_(njobs) {
-        if (!mailbox_on() || njobs < 2 || njobs > rsmi::kMailboxJobs || !rsmi::mailbox_supported(c->k, rows)) return;
+        if (!mailbox_on() || njobs < mailbox_min_jobs() || njobs > rsmi::kMailboxJobs ||
+            !rsmi::mailbox_supported(c->k, rows))
+            return;
         if (!L.mb) {
             void* h = nullptr;
             if (hipHostMalloc(&h, sizeof(rsmi::MailboxHost), hipHostMallocCoherent) != hipSuccess) return;
@@ -1389,13 +1404,15 @@ int stage_chunks(size_t bytes) {
     return bytes >= (size_t(256) << 10) ? 2 : 1;
 }
 // A two-chunk message splits at RSMI_FIRST_CHUNK_PCT percent of each shard
-// (default 50): a smaller first chunk is staged sooner, so the GPU starts
-// reading earlier while the host stages the rest.
+// (default 33): a smaller first chunk is staged sooner, so the GPU starts
+// reading earlier while the host stages the rest (config-1 decode / encode
+// 48.9-49.7 / 55.0-57.3 us at 50 %, 47.6-48.9 / 50.0-50.8 us at 33 %,
+// profiles/r06o/).
 size_t first_chunk_pct() {
     static const size_t pct = [] {
         const char* e = std::getenv("RSMI_FIRST_CHUNK_PCT");
-        const long v = e ? std::atol(e) : 50;
-        return static_cast<size_t>(v >= 10 && v <= 90 ? v : 50);
+        const long v = e ? std::atol(e) : 33;
+        return static_cast<size_t>(v >= 10 && v <= 90 ? v : 33);
     }();
     return pct;
 }
@@ -1554,7 +1571,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
         const size_t w = chunk_off(S, ch + 1, nch) - chunk_off(S, ch, nch);
         mb_blocks = std::max<uint32_t>(mb_blocks, static_cast<uint32_t>((round_up(w, 16) / 16 + 255) / 256 * ((e + 3) / 4)));
     }
-    MailboxCall mb(c, L, stage && !async_copies && L.chunk_stream(1) == s ? nch : 0, e, mb_blocks);
+    MailboxCall mb(c, L, !async_copies && L.chunk_stream(1) == s ? nch : 0, e, mb_blocks);
     // every chunk records its event unless RSMI_CHUNK_EVENTS=0 on one stream
     const bool ev_each = mb.ok() || chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t err = hipSuccess;
