@@ -837,6 +837,45 @@ def device_set_child(args, k, n, S):
     return json.loads(lines[-1])
 
 
+def _cpulist(text: str) -> set:
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def pin_to_gpu_numa(local: int):
+    """Runs the calling thread -- and the threads it starts later -- on the
+    CPUs of the NUMA node GPU `local` hangs off (sysfs numa_node of its PCI
+    function), as a deployment pins a GPU process.  The single-message legs
+    depend on it: a config-1 decode / encode from a thread on the GPU's node
+    took 47.6-48.2 / 50.9-52.1 us, from the other socket 59.8-60.1 / 64.2-64.5
+    us (profiles/r06q/).  The headline (device resident) does not.  Returns
+    what was done, for the JSON line; RSMI_BENCH_NO_PIN=1 leaves the
+    affinity alone."""
+    if os.environ.get("RSMI_BENCH_NO_PIN"):
+        return {"pinned": False, "why": "RSMI_BENCH_NO_PIN"}
+    try:
+        p = torch.cuda.get_device_properties(local)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as fh:
+            node = int(fh.read())
+        if node < 0:
+            return {"pinned": False, "gpu_pci": bdf, "why": "no NUMA node"}
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as fh:
+            cpus = _cpulist(fh.read()) & os.sched_getaffinity(0)
+        if not cpus:
+            return {"pinned": False, "gpu_pci": bdf, "gpu_numa_node": node, "why": "no allowed CPU on the node"}
+        os.sched_setaffinity(0, cpus)
+        return {"pinned": True, "gpu_pci": bdf, "gpu_numa_node": node, "cpus": len(cpus)}
+    except (OSError, ValueError, RuntimeError, AttributeError) as e:
+        return {"pinned": False, "why": repr(e)[:120]}
+
+
 def main():
     global _RESULT_OUT
     args = parse()
@@ -862,6 +901,7 @@ def main():
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
+    affinity = pin_to_gpu_numa(local)
     distributed = "RANK" in os.environ  # launched by torch.distributed.run (any N)
     if distributed:
         import torch.distributed as dist
@@ -962,6 +1002,7 @@ def main():
                 "k": k, "n": n, "shard_bytes": S, "stripes_per_gpu": stripes,
                 "data_bytes_per_gpu": stripes * k * S,
                 "parallelism": f"stripe-partitioned x{world}, no collective",
+                "host_affinity": affinity,
                 "erasure_patterns": "all" if pool == 0 else f"pool of {pool}",
                 "mode": args.mode,
             },

@@ -152,6 +152,7 @@ struct Staging {
     void* p = nullptr;
     void* dev = nullptr;  // p's device alias (queried once per allocation, not per call)
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;  // hipHostMallocWriteCombined: the host only ever writes it
     hipEvent_t done = nullptr;
     bool pending = false;
     std::vector<void*> retired;
@@ -164,7 +165,7 @@ struct Staging {
         if (bytes <= cap) return true;
         const size_t want = std::max({bytes, size_t(1) << 16, 2 * cap});
         void* np = nullptr;
-        if (hipHostMalloc(&np, want, hipHostMallocDefault) != hipSuccess) return false;
+        if (hipHostMalloc(&np, want, flags) != hipSuccess) return false;
         if (p) retired.push_back(p);
         p = np;
         if (hipHostGetDevicePointer(&dev, np, 0) != hipSuccess) dev = np;
@@ -243,6 +244,14 @@ struct Lease {
     uint64_t seen_tables = ~uint64_t(0);
 
     bool init() {
+        // RSMI_STAGE_WC=1: a single message's input staging in write-combined
+        // memory -- the host writes it with streaming stores only, and the
+        // kernel's PCIe reads of it need not snoop the CPU's caches.
+        static const bool wc = [] {
+            const char* e = std::getenv("RSMI_STAGE_WC");
+            return e && std::atoi(e) != 0;
+        }();
+        if (wc) st_in.flags = hipHostMallocWriteCombined;
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
         if (hipEventCreateWithFlags(&dev_done, hipEventDisableTiming) != hipSuccess) return false;
         for (hipEvent_t& e : ev)
@@ -1390,6 +1399,32 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                   bool present_done, int nch = 1, const StageFn& stage = nullptr);
 
 
+// Where a staged message's column chunks split, as cumulative percentages
+// of each shard: RSMI_CHUNK_SPLIT ("33" by default: two chunks, the first a
+// third -- staged sooner, so the GPU starts reading earlier while the host
+// stages the rest; config-1 decode / encode 48.9-49.7 / 55.0-57.3 us at 50 %,
+// 47.6-48.9 / 50.0-50.8 us at 33 %, profiles/r06o/).  A split of n cuts
+// applies to calls of n + 1 chunks (RSMI_STAGE_CHUNKS); other counts split
+// evenly.
+const std::vector<size_t>& chunk_split() {
+    static const std::vector<size_t> cuts = [] {
+        std::vector<size_t> v;
+        const char* e = std::getenv("RSMI_CHUNK_SPLIT");
+        const std::string str = e ? e : "33";
+        size_t prev = 0;
+        for (size_t i = 0; i < str.size();) {
+            const size_t j = std::min(str.find(',', i), str.size());
+            const long pct = std::atol(str.substr(i, j - i).c_str());
+            if (pct <= static_cast<long>(prev) || pct >= 100) return std::vector<size_t>{33};
+            v.push_back(static_cast<size_t>(pct));
+            prev = static_cast<size_t>(pct);
+            i = j + 1;
+        }
+        if (v.empty() || v.size() > 3) return std::vector<size_t>{33};
+        return v;
+    }();
+    return cuts;
+}
 // Column chunks of a staged small message: chunk c covers bytes
 // [off(c), off(c + 1)) of every shard, offsets multiples of 16.  Two chunks
 // let the host stage the second half while the kernel codes the first (and
@@ -1401,24 +1436,12 @@ int stage_chunks(size_t bytes) {
         return e ? std::max(1, std::min(std::atoi(e), 4)) : 0;
     }();
     if (forced) return forced;
-    return bytes >= (size_t(256) << 10) ? 2 : 1;
-}
-// A two-chunk message splits at RSMI_FIRST_CHUNK_PCT percent of each shard
-// (default 33): a smaller first chunk is staged sooner, so the GPU starts
-// reading earlier while the host stages the rest (config-1 decode / encode
-// 48.9-49.7 / 55.0-57.3 us at 50 %, 47.6-48.9 / 50.0-50.8 us at 33 %,
-// profiles/r06o/).
-size_t first_chunk_pct() {
-    static const size_t pct = [] {
-        const char* e = std::getenv("RSMI_FIRST_CHUNK_PCT");
-        const long v = e ? std::atol(e) : 33;
-        return static_cast<size_t>(v >= 10 && v <= 90 ? v : 33);
-    }();
-    return pct;
+    return bytes >= (size_t(256) << 10) ? static_cast<int>(chunk_split().size()) + 1 : 1;
 }
 size_t chunk_off(size_t S, int c, int nch) {
     if (c >= nch) return S;
-    if (nch == 2 && c == 1) return (S * first_chunk_pct() / 100) & ~size_t(15);
+    const std::vector<size_t>& cuts = chunk_split();
+    if (c > 0 && static_cast<size_t>(nch) == cuts.size() + 1) return (S * cuts[c - 1] / 100) & ~size_t(15);
     return (S * c / nch) & ~size_t(15);
 }
 

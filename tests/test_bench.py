@@ -241,3 +241,11 @@ def test_agree_max_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: (8, 1), 1: (8, 1)}, res
+
+
+def test_cpulist_and_pin_opt_out(monkeypatch):
+    import bench
+    assert bench._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert bench._cpulist("") == set()
+    monkeypatch.setenv("RSMI_BENCH_NO_PIN", "1")
+    assert bench.pin_to_gpu_numa(0) == {"pinned": False, "why": "RSMI_BENCH_NO_PIN"}

@@ -8,6 +8,14 @@ import os
 import sys
 import time
 
+if os.environ.get("RSMI_PIN_CPU"):  # before any HIP call: the calling thread's CPU (NUMA A/B runs)
+    os.sched_setaffinity(0, {int(os.environ["RSMI_PIN_CPU"])})
+elif os.environ.get("RSMI_PIN_GPU_NUMA"):  # the CPUs of the GPU's NUMA node, as bench.py runs
+    sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__)))]
+    import bench  # noqa: E402
+    bench.torch.cuda.set_device(0)
+    print("affinity", bench.pin_to_gpu_numa(0))
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "noise-erasurecode-plugin_amd")]
 import numpy as np  # noqa: E402
@@ -69,3 +77,9 @@ if what == "decode_batch":
 per = B if what.endswith("batch") else 1
 print(f"{what}: median {np.median(ts) * 1e6:.1f} us over {reps} calls ({np.median(ts) * 1e6 / per:.1f} us per message; "
       f"single-message drops {lost})")
+try:  # where the calling thread ran (NUMA A/B runs)
+    cpu = ctypes.CDLL(None).sched_getcpu()
+    node = [d for d in os.listdir(f"/sys/devices/system/cpu/cpu{cpu}") if d.startswith("node")]
+    print(f"cpu {cpu} {node[0] if node else 'node?'}")
+except OSError:
+    pass
