@@ -1400,36 +1400,40 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
 
 
 // Where a staged message's column chunks split, as cumulative percentages
-// of each shard: RSMI_CHUNK_SPLIT ("33" by default: two chunks, the first a
-// third -- staged sooner, so the GPU starts reading earlier while the host
-// stages the rest; config-1 decode / encode 48.9-49.7 / 55.0-57.3 us at 50 %,
-// 47.6-48.9 / 50.0-50.8 us at 33 %, profiles/r06o/).  A split of n cuts
-// applies to calls of n + 1 chunks (RSMI_STAGE_CHUNKS); other counts split
-// evenly.
+// of each shard: RSMI_CHUNK_SPLIT ("25,60" by default: three chunks of 25,
+// 35 and 40 % -- the first staged soon, so the GPU starts reading early,
+// each later one read by its own block group while the host stages the
+// next).  Config-1 decode / encode, caller on the GPU's NUMA node
+// (profiles/r06r/): "33" 46.8-47.4 / 50.4-51.0 us, "20,60" 46.0-47.7 /
+// 47.2-48.2, "15,50" 47.3 / 49.6-49.9, "25,60" 44.9-45.7 / 47.0-47.4; an
+// even split of two chunks was 48.9-49.7 / 55.0-57.3 (profiles/r06o/).  A
+// split of n cuts applies to calls of n + 1 chunks (RSMI_STAGE_CHUNKS
+// forces another count, split evenly).
 const std::vector<size_t>& chunk_split() {
     static const std::vector<size_t> cuts = [] {
         std::vector<size_t> v;
         const char* e = std::getenv("RSMI_CHUNK_SPLIT");
-        const std::string str = e ? e : "33";
+        const std::string str = e ? e : "25,60";
         size_t prev = 0;
         for (size_t i = 0; i < str.size();) {
             const size_t j = std::min(str.find(',', i), str.size());
             const long pct = std::atol(str.substr(i, j - i).c_str());
-            if (pct <= static_cast<long>(prev) || pct >= 100) return std::vector<size_t>{33};
+            if (pct <= static_cast<long>(prev) || pct >= 100) return std::vector<size_t>{25, 60};
             v.push_back(static_cast<size_t>(pct));
             prev = static_cast<size_t>(pct);
             i = j + 1;
         }
-        if (v.empty() || v.size() > 3) return std::vector<size_t>{33};
+        if (v.empty() || v.size() > 3) return std::vector<size_t>{25, 60};
         return v;
     }();
     return cuts;
 }
 // Column chunks of a staged small message: chunk c covers bytes
-// [off(c), off(c + 1)) of every shard, offsets multiples of 16.  Two chunks
-// let the host stage the second half while the kernel codes the first (and
-// copy the first half's outputs out while it codes the second);
-// RSMI_STAGE_CHUNKS overrides (1..4).
+// [off(c), off(c + 1)) of every shard, offsets multiples of 16.  Several
+// chunks let the host stage the later ones while the kernel codes the first
+// (and copy the first ones' outputs out while it codes the last): messages
+// of >= 256 KiB take chunk_split()'s count, RSMI_STAGE_CHUNKS overrides
+// (1..4).
 int stage_chunks(size_t bytes) {
     static const int forced = [] {
         const char* e = std::getenv("RSMI_STAGE_CHUNKS");
