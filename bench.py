@@ -399,29 +399,6 @@ def _median_ms(fn, reps):
 
 
 def config1_leg(local, reps=50):
-    """configs[0] (see _config1_leg) with the calling thread held on one CPU
-    -- the one it is on, inside the GPU's NUMA node when bench.py pinned the
-    process -- for the whole leg, GPU calls and the one-core oracle alike:
-    a latency-bound caller that hops between L3 domains meets its buffers
-    cold (RSMI_C1_PIN=node keeps the process-wide affinity)."""
-    import ctypes
-    saved = os.sched_getaffinity(0)
-    cpu = None
-    if os.environ.get("RSMI_C1_PIN", "cpu") == "cpu":
-        try:
-            cpu = ctypes.CDLL(None).sched_getcpu()
-            os.sched_setaffinity(0, {cpu})
-        except (OSError, AttributeError):
-            cpu = None
-    try:
-        out = _config1_leg(local, reps)
-    finally:
-        os.sched_setaffinity(0, saved)
-    out["caller_cpu"] = cpu
-    return out
-
-
-def _config1_leg(local, reps=50):
     """configs[0]: the reference's own per-message call pattern.  The
     1,048,580-B blob (1 MiB of splitmix64 bytes zero-padded to a multiple
     of k = 10) is encoded once per call the way

@@ -15,4 +15,4 @@ bench.torch.cuda.set_device(0)
 aff = bench.pin_to_gpu_numa(0)  # as bench.py does (RSMI_BENCH_NO_PIN=1: not)
 d = bench.config1_leg(0, reps)
 print(json.dumps({"codec": d.get("codec"), "cpu_1t": d.get("cpu_1t"), "gpu_vs_1core": d.get("gpu_vs_1core"),
-                  "host_affinity": aff, "caller_cpu": d.get("caller_cpu")}))
+                  "host_affinity": aff}))
