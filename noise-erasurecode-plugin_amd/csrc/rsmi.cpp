@@ -1393,6 +1393,35 @@ private:
 // Returns kDecodeNoStaging, having done nothing, when its pinned staging
 // cannot be had (the caller falls back to the pipeline).
 using StageFn = std::function<std::vector<rsmi::CopyPool::Piece>(size_t off, size_t w)>;
+
+// The present data shares into dst while a single message's kernels run,
+// on the calling thread: with streaming stores when the survivors were
+// staged (the GPU is reading the staging meanwhile), with memcpy when the
+// kernel reads engine-pinned survivors in place.  Config-1 decode, caller on
+// the GPU's node (profiles/r06t/): handing the copy to the pool (a wake-up,
+// parts claimed under its lock) 46.0-46.1 us, memcpy 44.8-46.2, streaming
+// stores 44.2-44.8; the arena decode 1.02-1.04x one core with the pool,
+// 1.05-1.06x with memcpy, 0.94-0.95x with streaming stores.
+// RSMI_PRESENT_COPY=pool|inline|nt forces one way for both (A/B).
+void copy_present_shares(const std::vector<rsmi::CopyPool::Piece>& v, size_t part, bool staged) {
+    static const int forced = [] {
+        const char* e = std::getenv("RSMI_PRESENT_COPY");
+        if (!e) return -1;
+        const std::string m(e);
+        return m == "pool" ? 0 : m == "inline" ? 1 : m == "nt" ? 2 : -1;
+    }();
+    const int mode = forced >= 0 ? forced : staged ? 2 : 1;
+    if (mode == 0) {
+        rsmi::CopyPool& pool = rsmi::CopyPool::shared();
+        pool.finish(pool.start(v, part));
+        return;
+    }
+    for (const rsmi::CopyPool::Piece& q : v) {
+        if (mode == 2) rsmi::stage_copy(q.dst, q.src, q.len);
+        else std::memcpy(q.dst, q.src, q.len);
+    }
+    if (mode == 2) rsmi::stage_fence();
+}
 constexpr int kDecodeNoStaging = -1000;
 int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, const std::vector<const uint8_t*>& by_id,
                   const std::vector<int>& surv, const std::vector<uint64_t>& dev, size_t S, uint8_t* dst,
@@ -1527,9 +1556,8 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
                 if (present[i] && dst + static_cast<size_t>(i) * S != by_id[i]) v.push_back({dst + static_cast<size_t>(i) * S, by_id[i], S});
         return v;
     };
-    if (e == 0) {
-        const std::vector<rsmi::CopyPool::Piece> v = present_pieces();
-        rsmi::CopyPool::shared().finish(rsmi::CopyPool::shared().start(v, S));
+    if (e == 0) {  // every data share present: copies only
+        copy_present_shares(present_pieces(), S, false);
         return RS_OK;
     }
     // dst never overlaps a share here: rs_decode sets aliasing shares aside
@@ -1644,7 +1672,7 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     L.end(s);
     for (rsmi::CopyPool::Async* j : staged) pool.finish(j);  // a failed launch left some unjoined
     if (async_copies) pool.finish(present_job);  // while the kernel runs
-    else pool.finish(pool.start(present_pieces(), S));
+    else copy_present_shares(present_pieces(), S, stage != nullptr);
     rsmi::trace_mark("copy_present");
     for (int ch = 0; ch < launched; ++ch) {
         if (!ev_each && ch < nch - 1) continue;  // no event of its own: copied out with the last chunk
