@@ -373,11 +373,13 @@ __device__ __forceinline__ uint64_t mb_clock() { return __builtin_amdgcn_s_memre
 
 template <int K, int MG, int BT>
 __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxDev* d, uint32_t per_job,
-                                                        uint64_t timeout) {
+                                                        uint64_t timeout, uint32_t stamps) {
     extern __shared__ uint4 lds4[];
     __shared__ MailboxJob job;
     __shared__ uint32_t go_s;
     const uint32_t j = blockIdx.x / per_job;  // this block's job, 0-based
+    const bool stamper = stamps && threadIdx.x == 0 && blockIdx.x == j * per_job;
+    if (stamps && threadIdx.x == 0 && blockIdx.x == 0) d->stamp[0] = mb_clock();
     if (threadIdx.x == 0) {
         uint32_t go = 0;
         const uint64_t since = mb_clock();
@@ -391,6 +393,7 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
             __builtin_amdgcn_s_sleep(4);
         }
         go_s = go;
+        if (stamper) d->stamp[1 + 3 * j] = mb_clock();
     }
     __syncthreads();
     if (go_s) {
@@ -404,6 +407,7 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
                 dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
+        if (stamper) d->stamp[2 + 3 * j] = mb_clock();
         const uint32_t nblk = job.blocks;
         for (uint32_t lb = blockIdx.x - j * per_job; lb < nblk; lb += per_job) {
             matmul_block<K, MG, BT, true>(job.a, lb, nblk, lds4);
@@ -413,8 +417,10 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
         if (threadIdx.x == 0 &&
-            __hip_atomic_fetch_add(&d->arrive[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == per_job)
+            __hip_atomic_fetch_add(&d->arrive[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == per_job) {
+            if (stamps) d->stamp[3 + 3 * j] = mb_clock();
             __hip_atomic_store(&h->done[j], static_cast<uint64_t>(j + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     // The last block out zeroes the device counters for the next launch on
     // this stream (kernel boundaries order the two).
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
 
 struct MailboxVariant {
     int K, MG;
-    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t);  // (h, d, per_job, timeout)
+    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t, uint32_t);  // (h, d, per_job, timeout, stamps)
 };
 const MailboxVariant kMailbox[] = {
     {10, 4, rs_mailbox_kernel<10, 4, 256>},  // RS(10,4): BASELINE config 1
@@ -531,12 +537,12 @@ void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job) {
 }
 
 hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t per_job,
-                          uint64_t timeout, hipStream_t stream) {
+                          uint64_t timeout, hipStream_t stream, bool stamps) {
     const MailboxVariant* v = mailbox_variant(k, rows);
     if (!v || per_job == 0 || njobs < 1 || njobs > kMailboxJobs) return hipErrorInvalidValue;
     const size_t lds = static_cast<size_t>(k) * ((v->MG + 3) / 4) * kStepWords * 4 + k * sizeof(void*);
     hipLaunchKernelGGL(v->fn, dim3(per_job * static_cast<uint32_t>(njobs)), dim3(kBlock), lds, stream, h, d, per_job,
-                       timeout);
+                       timeout, static_cast<uint32_t>(stamps));
     return hipGetLastError();
 }
 

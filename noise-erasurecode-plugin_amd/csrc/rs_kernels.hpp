@@ -81,6 +81,11 @@ struct MailboxDev {  // device memory: zero between launches (the grid's last bl
     uint32_t left;    // blocks that have left
     uint32_t arrive[kMailboxJobs];  // blocks of job j's group finished with it
     uint32_t pad[11];
+    // Diagnostics (launch_mailbox's stamps flag, RSMI_MAILBOX_STAMPS):
+    // device wall clock at block 0's entry, then per job when its group's
+    // first block saw it posted, had its arguments, and when the group's
+    // last block stored done.
+    uint64_t stamp[1 + 3 * kMailboxJobs];
 };
 
 // Whether a mailbox grid serves jobs of k survivors and up to `rows`
@@ -95,7 +100,7 @@ void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job);
 // an ordinary launch after the stream drained).  h is the device alias of
 // the MailboxHost.
 hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t per_job,
-                          uint64_t timeout, hipStream_t stream);
+                          uint64_t timeout, hipStream_t stream, bool stamps = false);
 
 // Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
 const char* variant_name(int k, int rows);  // kernel coding up to `rows` outputs per stripe

@@ -1270,6 +1270,51 @@ long mailbox_timeout_us() {
     return us;
 }
 
+// RSMI_MAILBOX_STAMPS=1 (diagnostics): every grid records device wall-clock
+// stamps (rs_kernels.hpp MailboxDev::stamp) and the caller its own post and
+// done times; medians go to stderr at exit.  Costs a synchronous copy per call.
+struct MailboxStamps {
+    std::mutex mu;
+    std::vector<std::vector<double>> cols;  // per metric
+    std::vector<std::string> names;
+    static MailboxStamps& get() {
+        static MailboxStamps* s = [] {
+            auto* p = new MailboxStamps;
+            std::atexit([] { get().print(); });
+            return p;
+        }();
+        return *s;
+    }
+    void add(const std::string& name, double us) {
+        std::lock_guard<std::mutex> lk(mu);
+        size_t i = 0;
+        while (i < names.size() && names[i] != name) ++i;
+        if (i == names.size()) {
+            names.push_back(name);
+            cols.emplace_back();
+        }
+        cols[i].push_back(us);
+    }
+    void print() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (names.empty()) return;
+        std::fprintf(stderr, "RSMI_MAILBOX_STAMPS %zu calls, median us (host: from the launch call's return; device: from block 0's entry):\n",
+                     cols[0].size());
+        for (size_t i = 0; i < names.size(); ++i) {
+            std::vector<double> v = cols[i];
+            std::sort(v.begin(), v.end());
+            std::fprintf(stderr, "  %-28s %8.2f\n", names[i].c_str(), v[v.size() / 2]);
+        }
+    }
+};
+bool mailbox_stamps() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSMI_MAILBOX_STAMPS");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 class MailboxCall {
 public:
     // Launches the grid for njobs jobs of up to `rows` outputs per stripe
@@ -1307,9 +1352,14 @@ public:
         for (uint64_t& d : h->done) __atomic_store_n(&d, uint64_t(0), __ATOMIC_RELAXED);
         __atomic_store_n(&h->posted, uint64_t(0), __ATOMIC_RELEASE);
         const uint32_t per_job = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 64));
-        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, njobs, c->k, rows, per_job, L.mb_timeout, L.stream) != hipSuccess) {
+        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, njobs, c->k, rows, per_job, L.mb_timeout, L.stream,
+                                 mailbox_stamps()) != hipSuccess) {
             (void)hipGetLastError();
             return;
+        }
+        if (mailbox_stamps()) {
+            t_launch_ = std::chrono::steady_clock::now();
+            khz_ = static_cast<double>(L.mb_timeout) / mailbox_timeout_us() * 1000.0;
         }
         ok_ = true;
         ++c->mailbox_calls;
@@ -1319,6 +1369,8 @@ public:
         if (waited_ < njobs_) {  // an early return: the grid leaves once it sees quit, then the stream drains
             __atomic_store_n(&L_.mb->quit, uint64_t(1), __ATOMIC_RELEASE);
             (void)hipStreamSynchronize(L_.stream);
+        } else if (mailbox_stamps() && !recovered_) {
+            record_stamps();
         }
     }
     bool ok() const { return ok_; }
@@ -1330,6 +1382,7 @@ public:
         max_e_[j] = max_e;
         __atomic_store_n(&L_.mb->posted, static_cast<uint64_t>(j + 1), __ATOMIC_RELEASE);
         posted_ = j + 1;
+        if (mailbox_stamps()) t_post_[j] = std::chrono::steady_clock::now();
     }
     // Waits for job j.  A grid that gave up (mailbox_timeout_us) or could
     // not run leaves jobs undone: after 2.5x that the caller asks it to
@@ -1351,10 +1404,33 @@ public:
             }
         }
         waited_ = std::max(waited_, j + 1);
+        if (mailbox_stamps()) t_done_[j] = std::chrono::steady_clock::now();
         return hipSuccess;
     }
 
 private:
+    void record_stamps() {
+        uint64_t st[1 + 3 * rsmi::kMailboxJobs] = {};
+        if (hipStreamSynchronize(L_.stream) != hipSuccess ||
+            hipMemcpy(st, L_.mbd->stamp, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess)
+            return;
+        MailboxStamps& ms = MailboxStamps::get();
+        auto host_us = [&](std::chrono::steady_clock::time_point t) {
+            return std::chrono::duration<double, std::micro>(t - t_launch_).count();
+        };
+        auto dev_us = [&](uint64_t a, uint64_t b) { return (static_cast<double>(b) - static_cast<double>(a)) * 1000.0 / khz_; };
+        for (int j = 0; j < njobs_; ++j) {
+            const std::string p = "job" + std::to_string(j) + " ";
+            ms.add(p + "host post", host_us(t_post_[j]));
+            ms.add(p + "host sees done", host_us(t_done_[j]));
+            ms.add(p + "dev seen posted", dev_us(st[0], st[1 + 3 * j]));
+            ms.add(p + "dev args loaded", dev_us(st[0], st[2 + 3 * j]));
+            ms.add(p + "dev done stored", dev_us(st[0], st[3 + 3 * j]));
+        }
+    }
+    std::chrono::steady_clock::time_point t_launch_, t_post_[rsmi::kMailboxJobs], t_done_[rsmi::kMailboxJobs];
+    double khz_ = 100000.0;
+
     hipError_t recover(int j) {
         __atomic_store_n(&L_.mb->quit, uint64_t(1), __ATOMIC_RELEASE);
         hipError_t e = hipStreamSynchronize(L_.stream);  // the grid has left
