@@ -364,18 +364,20 @@ __global__ __launch_bounds__(BT) void rs_matmul_kernel(MatArgs a) {
 // instead of each chunk paying the read latency ramp again (a kernel reading
 // 256 KiB / 512 KiB / 1 MiB of pinned host memory takes 11 / 17 / 30 us,
 // profiles/r06n/pcie_rates.txt).  The last block of a group to finish
-// writes done[j - 1].  The call's chunks then cost the host a 0.3 KiB write
-// each instead of a launch and an event, and the grid's dispatch overlaps the
+// writes done[j - 1].  The call's chunks then cost the host one word each
+// instead of a launch and an event, and the grid's dispatch overlaps the
 // staging of the first chunk (profiles/r06h/: 4.3 us to launch a chunk,
-// 5 us to dispatch it, 5.4 us between two chunks' kernels).  Every wave
-// leaves: after its job, on quit, or when its job is not posted in time.
+// 5 us to dispatch it, 5.4 us between two chunks' kernels).  The jobs'
+// arguments ride in the kernel arguments: read from the job board in pinned
+// memory they cost each group 1.6-3.5 us of PCIe round trips before its
+// first survivor load (profiles/r06u/).  Every wave leaves: after its job,
+// on quit, or when its job is not posted in time.
 __device__ __forceinline__ uint64_t mb_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
 template <int K, int MG, int BT>
 __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxDev* d, uint32_t per_job,
-                                                        uint64_t timeout, uint32_t stamps) {
+                                                        uint64_t timeout, uint32_t stamps, MailboxJobs jobs) {
     extern __shared__ uint4 lds4[];
-    __shared__ MailboxJob job;
     __shared__ uint32_t go_s;
     const uint32_t j = blockIdx.x / per_job;  // this block's job, 0-based
     const bool stamper = stamps && threadIdx.x == 0 && blockIdx.x == j * per_job;
@@ -397,17 +399,12 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
     }
     __syncthreads();
     if (go_s) {
-        // Job j's arguments and inputs are in host memory the host wrote
-        // before posting it: nothing cached from earlier may be used.
+        // Job j's inputs (and a decode's pattern table) are in host memory
+        // the host wrote before posting it: nothing cached from earlier may
+        // be used.
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(&h->jobs[j]);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(&job);
-            for (uint32_t i = threadIdx.x; i < sizeof(MailboxJob) / 4; i += BT)
-                dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __syncthreads();
         if (stamper) d->stamp[2 + 3 * j] = mb_clock();
+        const MailboxJob& job = jobs.job[j];
         const uint32_t nblk = job.blocks;
         for (uint32_t lb = blockIdx.x - j * per_job; lb < nblk; lb += per_job) {
             matmul_block<K, MG, BT, true>(job.a, lb, nblk, lds4);
@@ -434,7 +431,7 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
 
 struct MailboxVariant {
     int K, MG;
-    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t, uint32_t);  // (h, d, per_job, timeout, stamps)
+    void (*fn)(MailboxHost*, MailboxDev*, uint32_t, uint64_t, uint32_t, MailboxJobs);  // (h, d, per_job, timeout, stamps, jobs)
 };
 const MailboxVariant kMailbox[] = {
     {10, 4, rs_mailbox_kernel<10, 4, 256>},  // RS(10,4): BASELINE config 1
@@ -536,13 +533,13 @@ void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job) {
     job->blocks = static_cast<uint32_t>(a.stripes * job->a.chunks * job->a.groups);
 }
 
-hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t per_job,
-                          uint64_t timeout, hipStream_t stream, bool stamps) {
+hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, const MailboxJobs& jobs, int njobs, int k, int rows,
+                          uint32_t per_job, uint64_t timeout, hipStream_t stream, bool stamps) {
     const MailboxVariant* v = mailbox_variant(k, rows);
     if (!v || per_job == 0 || njobs < 1 || njobs > kMailboxJobs) return hipErrorInvalidValue;
     const size_t lds = static_cast<size_t>(k) * ((v->MG + 3) / 4) * kStepWords * 4 + k * sizeof(void*);
     hipLaunchKernelGGL(v->fn, dim3(per_job * static_cast<uint32_t>(njobs)), dim3(kBlock), lds, stream, h, d, per_job,
-                       timeout, static_cast<uint32_t>(stamps));
+                       timeout, static_cast<uint32_t>(stamps), jobs);
     return hipGetLastError();
 }
 

@@ -58,24 +58,27 @@ hipError_t launch_matmul(MatArgs a, int max_e, hipStream_t stream);
 
 // Mailbox grid (rs_encode / rs_decode of one small message): one launch per
 // call of the split-table kernel, a group of blocks per column-chunk job,
-// each group coding its job as soon as the host has staged and posted it --
-// instead of a launch, a dispatch and a completion event per chunk.  The
-// host writes job j (1-based) into jobs[j - 1], then posted = j; job j's
-// group codes it and writes done[j - 1] = j.  quit (host) makes the groups
-// still waiting for their job leave.
+// each group coding its job as soon as the host has staged it and bumped
+// `posted` -- instead of a launch, a dispatch and a completion event per
+// chunk.  Every job's arguments are known before the staging starts and go
+// in the launch's kernel arguments; the host's post is one word, and job j's
+// group writes done[j - 1] = j.  quit (host) makes the groups still waiting
+// for their job leave.
 constexpr int kMailboxJobs = 4;
 struct MailboxJob {
     MatArgs a;        // chunks / groups / iters planned (plan_mailbox_job), xcd 0
     uint32_t blocks;  // logical blocks of the job
     uint32_t pad[3];
 };
+struct MailboxJobs {  // by value in the kernel arguments
+    MailboxJob job[kMailboxJobs];
+};
 struct MailboxHost {  // pinned (coherent), device-mapped; read by the grid with system-scope loads
-    uint64_t posted;  // host: jobs posted so far
+    uint64_t posted;  // host: jobs posted (staged) so far
     uint64_t quit;    // host: nonzero = groups still waiting leave
     uint64_t pad0[14];
     uint64_t done[kMailboxJobs];  // grid: done[j - 1] = j once job j is coded
     uint64_t pad1[12];
-    MailboxJob jobs[kMailboxJobs];
 };
 struct MailboxDev {  // device memory: zero between launches (the grid's last block out zeroes it)
     uint32_t left;    // blocks that have left
@@ -93,14 +96,14 @@ struct MailboxDev {  // device memory: zero between launches (the grid's last bl
 bool mailbox_supported(int k, int rows);
 // Fills job->a's launch plan (as launch_matmul would) and job->blocks.
 void plan_mailbox_job(const MatArgs& a, int max_e, MailboxJob* job);
-// Launches njobs (1..kMailboxJobs) groups of per_job blocks (a group codes
-// its job's logical blocks in turn).  A block waits at most `timeout` device
+// Launches njobs (1..kMailboxJobs) groups of per_job blocks for jobs[0 ..
+// njobs) (a group codes its job's logical blocks in turn).  A block waits at most `timeout` device
 // wall-clock ticks (hipDeviceAttributeWallClockRate) for its job to be
 // posted; a job whose group gave up stays undone (the caller codes it with
 // an ordinary launch after the stream drained).  h is the device alias of
 // the MailboxHost.
-hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, int njobs, int k, int rows, uint32_t per_job,
-                          uint64_t timeout, hipStream_t stream, bool stamps = false);
+hipError_t launch_mailbox(MailboxHost* h, MailboxDev* d, const MailboxJobs& jobs, int njobs, int k, int rows,
+                          uint32_t per_job, uint64_t timeout, hipStream_t stream, bool stamps = false);
 
 // Which compiled variant serves (k, m): "K10_MG4" etc. (diagnostics).
 const char* variant_name(int k, int rows);  // kernel coding up to `rows` outputs per stripe

@@ -1317,13 +1317,19 @@ bool mailbox_stamps() {
 
 class MailboxCall {
 public:
-    // Launches the grid for njobs jobs of up to `rows` outputs per stripe
-    // and `blocks` logical blocks each on L.stream (after L.begin), or
-    // leaves ok() false: the caller launches its chunks itself.
-    MailboxCall(rs_ctx* c, Lease& L, int njobs, int rows, uint32_t blocks) : c_(c), L_(L), njobs_(njobs) {
-        if (!mailbox_on() || njobs < mailbox_min_jobs() || njobs > rsmi::kMailboxJobs ||
-            !rsmi::mailbox_supported(c->k, rows))
+    // Launches the grid for the chunks' launch arguments `args` (up to
+    // max_e outputs per stripe) on L.stream (after L.begin), or leaves ok()
+    // false: the caller launches its chunks itself.  `use` false: off.
+    MailboxCall(rs_ctx* c, Lease& L, bool use, const std::vector<rsmi::MatArgs>& args, int max_e)
+        : c_(c), L_(L), njobs_(static_cast<int>(args.size())), max_e_(max_e) {
+        if (!use || !mailbox_on() || njobs_ < mailbox_min_jobs() || njobs_ > rsmi::kMailboxJobs ||
+            !rsmi::mailbox_supported(c->k, max_e))
             return;
+        uint32_t blocks = 1;
+        for (int j = 0; j < njobs_; ++j) {
+            rsmi::plan_mailbox_job(args[static_cast<size_t>(j)], max_e, &jobs_.job[j]);
+            blocks = std::max(blocks, jobs_.job[j].blocks);
+        }
         if (!L.mb) {
             void* h = nullptr;
             if (hipHostMalloc(&h, sizeof(rsmi::MailboxHost), hipHostMallocCoherent) != hipSuccess) return;
@@ -1351,8 +1357,8 @@ public:
         __atomic_store_n(&h->quit, uint64_t(0), __ATOMIC_RELAXED);
         for (uint64_t& d : h->done) __atomic_store_n(&d, uint64_t(0), __ATOMIC_RELAXED);
         __atomic_store_n(&h->posted, uint64_t(0), __ATOMIC_RELEASE);
-        const uint32_t per_job = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 64));
-        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, njobs, c->k, rows, per_job, L.mb_timeout, L.stream,
+        const uint32_t per_job = std::min<uint32_t>(blocks, 64);
+        if (rsmi::launch_mailbox(L.mb_dev, L.mbd, jobs_, njobs_, c->k, max_e, per_job, L.mb_timeout, L.stream,
                                  mailbox_stamps()) != hipSuccess) {
             (void)hipGetLastError();
             return;
@@ -1374,12 +1380,8 @@ public:
         }
     }
     bool ok() const { return ok_; }
-    // Job j (0-based): its arguments into the board, then the post.
-    void post(int j, const rsmi::MatArgs& a, int max_e) {
-        rsmi::MailboxJob job;
-        rsmi::plan_mailbox_job(a, max_e, &job);
-        std::memcpy(&L_.mb->jobs[j], &job, sizeof(job));
-        max_e_[j] = max_e;
+    // Job j (0-based) is staged: its group may start.
+    void post(int j) {
         __atomic_store_n(&L_.mb->posted, static_cast<uint64_t>(j + 1), __ATOMIC_RELEASE);
         posted_ = j + 1;
         if (mailbox_stamps()) t_post_[j] = std::chrono::steady_clock::now();
@@ -1436,8 +1438,7 @@ private:
         hipError_t e = hipStreamSynchronize(L_.stream);  // the grid has left
         for (int i = 0; i < posted_ && e == hipSuccess; ++i)
             if (__atomic_load_n(&L_.mb->done[i], __ATOMIC_ACQUIRE) != static_cast<uint64_t>(i + 1)) {
-                rsmi::MatArgs a = L_.mb->jobs[i].a;
-                e = rsmi::launch_matmul(a, max_e_[i], L_.stream);
+                e = rsmi::launch_matmul(jobs_.job[i].a, max_e_, L_.stream);
                 if (e == hipSuccess) __atomic_store_n(&L_.mb->done[i], static_cast<uint64_t>(i + 1), __ATOMIC_RELAXED);
             }
         if (e == hipSuccess) e = hipStreamSynchronize(L_.stream);
@@ -1452,8 +1453,9 @@ private:
     Lease& L_;
     int njobs_;
     bool ok_ = false, recovered_ = false;
+    int max_e_;
+    rsmi::MailboxJobs jobs_{};
     int posted_ = 0, waited_ = 0;
-    int max_e_[rsmi::kMailboxJobs] = {};
 };
 
 // The one-launch decode of decode_in_place / decode_staged: survivor j of
@@ -1695,14 +1697,29 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
     }
     L.begin(s);
     if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
-    // A staged message's chunks go to a mailbox grid launched now, whose
-    // dispatch overlaps the staging of chunk 0 (MailboxCall).
-    uint32_t mb_blocks = 0;
+    // Every chunk's launch arguments (and shard table) up front: a staged
+    // message's chunks go to a mailbox grid launched now, whose dispatch
+    // overlaps the staging of chunk 0 (MailboxCall).
+    std::vector<rsmi::MatArgs> args(static_cast<size_t>(nch));
     for (int ch = 0; ch < nch; ++ch) {
-        const size_t w = chunk_off(S, ch + 1, nch) - chunk_off(S, ch, nch);
-        mb_blocks = std::max<uint32_t>(mb_blocks, static_cast<uint32_t>((round_up(w, 16) / 16 + 255) / 256 * ((e + 3) / 4)));
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        rsmi::MatArgs& a = args[static_cast<size_t>(ch)];
+        a = strided ? base_args(c, reinterpret_cast<void*>(dev[0] + off), 0, reinterpret_cast<void*>(oalias + off), 0,
+                                span, w, 1)
+                    : base_args(c, nullptr, 0, nullptr, 0, span, w, 1);
+        set_patterns(c, 1, pat, a);
+        a.src = nullptr;                    // survivor j is id j, output t is id k + t
+        a.desc0 = static_cast<uint32_t>(e);  // pattern 0, e outputs
+        if (!strided) {
+            uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff + ch * n8);
+            for (int jj = 0; jj < k; ++jj) tab[jj] = dev[jj] + off;
+            for (int t = 0; t < e; ++t)
+                tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span) + off
+                                        : oalias + static_cast<uint64_t>(t) * span + off;
+            a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
+        }
     }
-    MailboxCall mb(c, L, !async_copies && L.chunk_stream(1) == s ? nch : 0, e, mb_blocks);
+    MailboxCall mb(c, L, !async_copies && L.chunk_stream(1) == s, args, e);
     // every chunk records its event unless RSMI_CHUNK_EVENTS=0 on one stream
     const bool ev_each = mb.ok() || chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t err = hipSuccess;
@@ -1721,24 +1738,10 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
             }
         }
         rsmi::trace_mark(ch ? "stage1" : "stage0");
-        rsmi::MatArgs a = strided ? base_args(c, reinterpret_cast<void*>(dev[0] + off), 0,
-                                              reinterpret_cast<void*>(oalias + off), 0, span, w, 1)
-                                  : base_args(c, nullptr, 0, nullptr, 0, span, w, 1);
-        set_patterns(c, 1, pat, a);
-        a.src = nullptr;                    // survivor j is id j, output t is id k + t
-        a.desc0 = static_cast<uint32_t>(e);  // pattern 0, e outputs
-        if (!strided) {
-            uint64_t* tab = reinterpret_cast<uint64_t*>(host + toff + ch * n8);
-            for (int jj = 0; jj < k; ++jj) tab[jj] = dev[jj] + off;
-            for (int t = 0; t < e; ++t)
-                tab[k + t] = dst_direct ? rsmi::pinned_device_address(dst + static_cast<size_t>(missing[t]) * S, span) + off
-                                        : oalias + static_cast<uint64_t>(t) * span + off;
-            a.shard_ptrs = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(halias) + toff + ch * n8);
-        }
         if (mb.ok()) {
-            mb.post(ch, a, e);
+            mb.post(ch);
         } else {
-            err = rsmi::launch_matmul(a, e, cs);
+            err = rsmi::launch_matmul(args[static_cast<size_t>(ch)], e, cs);
             if (err == hipSuccess && (ev_each || ch == nch - 1)) err = hipEventRecord(L.ev[ch], cs);
         }
         if (err == hipSuccess) ++launched;
@@ -1799,18 +1802,19 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
         for (int ch = 1; ch < nch; ++ch) staged[ch] = pool.start(pieces(ch), size_t(128) << 10);
     L.begin(s);
     if (nch > 1 && L.chunk_stream(1) != s) L.begin(L.chunk_stream(1));
-    uint32_t mb_blocks = 0;
+    std::vector<rsmi::MatArgs> args(static_cast<size_t>(nch));
     for (int ch = 0; ch < nch; ++ch) {
-        const size_t w = chunk_off(S, ch + 1, nch) - chunk_off(S, ch, nch);
-        mb_blocks = std::max<uint32_t>(mb_blocks, static_cast<uint32_t>((round_up(w, 16) / 16 + 255) / 256 * ((m + 3) / 4)));
+        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
+        rsmi::MatArgs& a = args[static_cast<size_t>(ch)];
+        a = base_args(c, static_cast<uint8_t*>(din) + off, 0, static_cast<uint8_t*>(dout) + off, 0, span, w, 1);
+        set_patterns(c, 1, c->d_encpat.p, a);
+        a.stripe_desc = nullptr;
     }
-    MailboxCall mb(c, L, !c->bitslice && !async_copies && L.chunk_stream(1) == s ? nch : 0, static_cast<int>(m),
-                   mb_blocks);
+    MailboxCall mb(c, L, !c->bitslice && !async_copies && L.chunk_stream(1) == s, args, static_cast<int>(m));
     const bool ev_each = mb.ok() || chunk_events() || (nch > 1 && L.chunk_stream(1) != s);
     hipError_t e = hipSuccess;
     int launched = 0;
     for (int ch = 0; ch < nch && e == hipSuccess; ++ch) {
-        const size_t off = chunk_off(S, ch, nch), w = chunk_off(S, ch + 1, nch) - off;
         const hipStream_t cs = L.chunk_stream(ch);
         if (staged[ch]) {
             pool.finish(staged[ch]);
@@ -1820,13 +1824,10 @@ bool encode_staged(rs_ctx* c, Lease& L, const uint8_t* input, size_t S, uint8_t*
             rsmi::stage_fence();
         }
         rsmi::trace_mark(ch ? "stage1" : "stage0");
-        rsmi::MatArgs a = base_args(c, static_cast<uint8_t*>(din) + off, 0, static_cast<uint8_t*>(dout) + off, 0, span, w, 1);
-        set_patterns(c, 1, c->d_encpat.p, a);
-        a.stripe_desc = nullptr;
         if (mb.ok()) {
-            mb.post(ch, a, static_cast<int>(m));
+            mb.post(ch);
         } else {
-            e = launch_encode(c, a, cs);
+            e = launch_encode(c, args[static_cast<size_t>(ch)], cs);
             if (e == hipSuccess && (ev_each || ch == nch - 1)) e = hipEventRecord(L.ev[ch], cs);
         }
         if (e == hipSuccess) ++launched;
