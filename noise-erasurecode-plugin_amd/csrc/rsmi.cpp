@@ -1507,30 +1507,33 @@ int decode_launch(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present, cons
 
 
 // Where a staged message's column chunks split, as cumulative percentages
-// of each shard: RSMI_CHUNK_SPLIT ("25,60" by default: three chunks of 25,
-// 35 and 40 % -- the first staged soon, so the GPU starts reading early,
+// of each shard: RSMI_CHUNK_SPLIT ("30,65" by default: three chunks of 30,
+// 35 and 35 % -- the first staged soon, so the GPU starts reading early,
 // each later one read by its own block group while the host stages the
-// next).  Config-1 decode / encode, caller on the GPU's NUMA node
-// (profiles/r06r/): "33" 46.8-47.4 / 50.4-51.0 us, "20,60" 46.0-47.7 /
-// 47.2-48.2, "15,50" 47.3 / 49.6-49.9, "25,60" 44.9-45.7 / 47.0-47.4; an
-// even split of two chunks was 48.9-49.7 / 55.0-57.3 (profiles/r06o/).  A
-// split of n cuts applies to calls of n + 1 chunks (RSMI_STAGE_CHUNKS
-// forces another count, split evenly).
+// next).  Config-1 decode / encode, caller on the GPU's NUMA node, jobs'
+// arguments in the kernel arguments (profiles/r06w/, three processes
+// each): "30,65" 42.1-42.8 / 44.5-45.6 us, "25,60" 42.9-43.8 / 44.9-46.2,
+// "25,55,80" 42.6-44.0 / 45.4-46.6, "20,50,80" 43.7-44.1 / 45.1-46.9;
+// earlier, with the arguments on the job board (profiles/r06r/): "33"
+// 46.8-47.4 / 50.4-51.0, "15,50" 47.3 / 49.6-49.9; an even split of two
+// chunks 48.9-49.7 / 55.0-57.3 (profiles/r06o/).  A split of n cuts applies
+// to calls of n + 1 chunks (RSMI_STAGE_CHUNKS forces another count, split
+// evenly).
 const std::vector<size_t>& chunk_split() {
     static const std::vector<size_t> cuts = [] {
         std::vector<size_t> v;
         const char* e = std::getenv("RSMI_CHUNK_SPLIT");
-        const std::string str = e ? e : "25,60";
+        const std::string str = e ? e : "30,65";
         size_t prev = 0;
         for (size_t i = 0; i < str.size();) {
             const size_t j = std::min(str.find(',', i), str.size());
             const long pct = std::atol(str.substr(i, j - i).c_str());
-            if (pct <= static_cast<long>(prev) || pct >= 100) return std::vector<size_t>{25, 60};
+            if (pct <= static_cast<long>(prev) || pct >= 100) return std::vector<size_t>{30, 65};
             v.push_back(static_cast<size_t>(pct));
             prev = static_cast<size_t>(pct);
             i = j + 1;
         }
-        if (v.empty() || v.size() > 3) return std::vector<size_t>{25, 60};
+        if (v.empty() || v.size() > 3) return std::vector<size_t>{30, 65};
         return v;
     }();
     return cuts;
