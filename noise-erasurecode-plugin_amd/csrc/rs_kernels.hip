@@ -395,6 +395,8 @@ __global__ __launch_bounds__(BT) void rs_mailbox_kernel(MailboxHost* h, MailboxD
             __builtin_amdgcn_s_sleep(4);
         }
         go_s = go;
+        if (!go)  // the waiting caller launches the job itself at once, not after its own deadline
+            __hip_atomic_store(&h->gave_up, uint64_t(1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (stamper) d->stamp[1 + 3 * j] = mb_clock();
     }
     __syncthreads();

@@ -78,7 +78,8 @@ struct MailboxHost {  // pinned (coherent), device-mapped; read by the grid with
     uint64_t quit;    // host: nonzero = groups still waiting leave
     uint64_t pad0[14];
     uint64_t done[kMailboxJobs];  // grid: done[j - 1] = j once job j is coded
-    uint64_t pad1[12];
+    uint64_t gave_up;             // grid: nonzero once a group left without its job (timeout or quit)
+    uint64_t pad1[11];
 };
 struct MailboxDev {  // device memory: zero between launches (the grid's last block out zeroes it)
     uint32_t left;    // blocks that have left

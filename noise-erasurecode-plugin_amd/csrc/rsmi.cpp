@@ -1355,6 +1355,7 @@ public:
         // all waited for, or it was drained): reset it for this one.
         rsmi::MailboxHost* h = L.mb;
         __atomic_store_n(&h->quit, uint64_t(0), __ATOMIC_RELAXED);
+        __atomic_store_n(&h->gave_up, uint64_t(0), __ATOMIC_RELAXED);
         for (uint64_t& d : h->done) __atomic_store_n(&d, uint64_t(0), __ATOMIC_RELAXED);
         __atomic_store_n(&h->posted, uint64_t(0), __ATOMIC_RELEASE);
         const uint32_t per_job = std::min<uint32_t>(blocks, 64);
@@ -1386,9 +1387,11 @@ public:
         posted_ = j + 1;
         if (mailbox_stamps()) t_post_[j] = std::chrono::steady_clock::now();
     }
-    // Waits for job j.  A grid that gave up (mailbox_timeout_us) or could
-    // not run leaves jobs undone: after 2.5x that the caller asks it to
-    // leave, drains the stream and launches what is still undone itself.
+    // Waits for job j.  A group that gave up (mailbox_timeout_us: the host
+    // was slow to post) says so in gave_up, and one that could not run at
+    // all leaves its job undone: then -- at once, or after 2.5x the timeout
+    // -- the caller asks the grid to leave, drains the stream and launches
+    // what is still undone itself.
     hipError_t wait(int j) {
         const uint64_t want = static_cast<uint64_t>(j + 1);
         const uint64_t* done = &L_.mb->done[j];
@@ -1400,6 +1403,7 @@ public:
                     __builtin_ia32_pause();
                     continue;
                 }
+                if (__atomic_load_n(&L_.mb->gave_up, __ATOMIC_ACQUIRE)) return recover(j);
                 const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
                 if (us > std::max(1000L, mailbox_timeout_us() * 5 / 2)) return recover(j);
                 if (us > 200) std::this_thread::sleep_for(std::chrono::microseconds(20));
