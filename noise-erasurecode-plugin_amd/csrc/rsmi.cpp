@@ -192,6 +192,7 @@ struct Staging {
 // rs_decode_batch moves survivors in / regenerated shards out in up to
 // kBatchChunks pieces once a direction carries kBatchChunkMin bytes.
 constexpr size_t kBatchChunks = 4;
+constexpr size_t kBatchChunksMax = 8;  // the direct batch forms' cap (RSMI_BATCH_CHUNKS); events per lease
 constexpr size_t kBatchChunkMin = size_t(16) << 20;
 
 // An erasure pattern as a 256-bit set of shard ids (n <= 256).
@@ -217,7 +218,7 @@ struct Lease {
     hipStream_t stream2 = nullptr;
     hipEvent_t dev_done = nullptr;
     std::atomic<bool> dev_pending{false};
-    hipEvent_t ev[kBatchChunks] = {};  // rs_decode_batch D2H chunk events
+    hipEvent_t ev[kBatchChunksMax] = {};  // per-chunk events (single messages, batches)
     Staging st_stripe;                 // stripe descriptors
     Staging st_batch, st_pieces;       // rs_decode_batch
     Staging st_onepat;                 // host-API decode: the one-pattern table, read in place by the kernel
@@ -2631,8 +2632,13 @@ size_t batch_stage_cap() {
 // -- two config-1 messages already run as two chunks, the first coded while
 // the second is staged (the single-message path's two-chunk overlap).
 size_t direct_batch_chunks(size_t messages, size_t in_bytes) {
+    static const size_t cap = [] {
+        const char* e = std::getenv("RSMI_BATCH_CHUNKS");
+        const long v = e ? std::atol(e) : static_cast<long>(kBatchChunks);
+        return static_cast<size_t>(std::max(1L, std::min(v, static_cast<long>(kBatchChunksMax))));
+    }();
     const size_t by_bytes = std::max<size_t>(1, in_bytes / (size_t(256) << 10));
-    return std::max<size_t>(1, std::min({messages, kBatchChunks, by_bytes}));
+    return std::max<size_t>(1, std::min({messages, cap, by_bytes}));
 }
 }  // namespace
 
@@ -2883,11 +2889,13 @@ int rs_decode_batch(rs_ctx* c, int batch, const int* counts, int* numbers, const
                 rows_before[j + 1] = rows_before[j] + e_j;
             }
             size_t launched = 0;
-            static const char* const kStage[] = {"stage0", "stage1", "stage2", "stage3"};
-            static const char* const kLaunch[] = {"launch0", "launch1", "launch2", "launch3"};
-            static const char* const kWait[] = {"wait0", "wait1", "wait2", "wait3"};
-            static const char* const kOut[] = {"copyout0", "copyout1", "copyout2", "copyout3"};
-            static_assert(kBatchChunks == 4, "trace phase names");
+            static const char* const kStage[] = {"stage0", "stage1", "stage2", "stage3", "stage4", "stage5", "stage6", "stage7"};
+            static const char* const kLaunch[] = {"launch0", "launch1", "launch2", "launch3",
+                                                  "launch4", "launch5", "launch6", "launch7"};
+            static const char* const kWait[] = {"wait0", "wait1", "wait2", "wait3", "wait4", "wait5", "wait6", "wait7"};
+            static const char* const kOut[] = {"copyout0", "copyout1", "copyout2", "copyout3",
+                                               "copyout4", "copyout5", "copyout6", "copyout7"};
+            static_assert(kBatchChunksMax == 8, "trace phase names");
             for (size_t ch = 0; ch < nch; ++ch) {
                 const size_t j0 = B * ch / nch, j1 = B * (ch + 1) / nch;
                 if (!in_place)
