@@ -1586,7 +1586,15 @@ bool decode_in_place(rs_ctx* c, Lease& L, const std::vector<uint8_t>& present,
         dev[j] = rsmi::pinned_device_address(p, span);
         if (!dev[j]) return false;
     }
-    const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false);
+    // RSMI_INPLACE_CHUNKS=1 (A/B): the column chunks of a staged message
+    // here too -- with the mailbox grid, a group per chunk and each chunk's
+    // rows copied out while the later ones are read.
+    static const bool chunked = [] {
+        const char* e = std::getenv("RSMI_INPLACE_CHUNKS");
+        return e && std::atoi(e) != 0;
+    }();
+    const int r = decode_launch(c, L, present, by_id, surv, dev, S, dst, false,
+                                chunked ? stage_chunks(static_cast<size_t>(k) * S) : 1);
     if (r == kDecodeNoStaging) return false;
     *rc = r;
     ++c->decodes_in_place;
