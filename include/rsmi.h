@@ -265,10 +265,15 @@ void *rs_pinned_alloc(size_t bytes); /* NULL on failure */
 void rs_pinned_free(void *p);
 /* Receive arena: one pinned range carved into 256-byte aligned slots by a
  * bump pointer (rs_shard_unmarshal_arena places ShardData in it).  Reset
- * recycles every slot; not thread-safe (one arena per receiving thread). */
+ * recycles every slot; not thread-safe (one arena per receiving thread).
+ * rs_arena_put copies bytes into a fresh slot with streaming stores, as
+ * rs_shard_unmarshal_arena does: the lines go to DRAM instead of staying
+ * dirty in the CPU's caches, where each of the kernel's PCIe reads would
+ * have to snoop them out. */
 typedef struct rs_arena rs_arena;
 rs_arena *rs_arena_new(size_t bytes);            /* NULL on failure */
 void *rs_arena_alloc(rs_arena *a, size_t bytes); /* NULL when full */
+void *rs_arena_put(rs_arena *a, const void *data, size_t bytes); /* the slot, NULL when full */
 void rs_arena_reset(rs_arena *a);
 size_t rs_arena_used(const rs_arena *a);
 void rs_arena_free(rs_arena *a);

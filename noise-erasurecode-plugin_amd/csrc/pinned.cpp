@@ -11,6 +11,7 @@
 #include <shared_mutex>
 
 #include "../../include/rsmi.h"
+#include "host_pipeline.hpp"
 
 namespace rsmi {
 namespace {
@@ -95,6 +96,16 @@ void* rs_arena_alloc(rs_arena* a, size_t bytes) {
     void* p = a->base + a->used;
     a->used += want;
     return p;
+}
+
+void* rs_arena_put(rs_arena* a, const void* data, size_t bytes) {
+    if (bytes && !data) return nullptr;
+    void* slot = rs_arena_alloc(a, bytes);
+    if (slot && bytes) {
+        rsmi::stage_copy(slot, data, bytes);
+        rsmi::stage_fence();
+    }
+    return slot;
 }
 
 void rs_arena_reset(rs_arena* a) {

@@ -195,9 +195,8 @@ int rs_shard_unmarshal_arena(const uint8_t* buf, size_t len, rs_arena* arena, rs
     if (!arena) return RS_EINVAL;
     const int rc = rs_shard_unmarshal(buf, len, out);
     if (rc != 0 || out->shard_data_len == 0) return rc;
-    void* slot = rs_arena_alloc(arena, out->shard_data_len);
+    void* slot = rs_arena_put(arena, out->shard_data, out->shard_data_len);  // streaming stores
     if (!slot) return RS_ENOMEM;
-    std::memcpy(slot, out->shard_data, out->shard_data_len);
     out->shard_data = static_cast<const uint8_t*>(slot);
     return 0;
 }

@@ -425,6 +425,21 @@ func (a *Arena) Reset() { C.rs_arena_reset(a.a) }
 // Free releases the arena's pinned memory.
 func (a *Arena) Free() { C.rs_arena_free(a.a); a.a = nil }
 
+// Put copies a share's bytes into a fresh slot (rs_arena_put: streaming
+// stores, so the GPU's reads need not snoop the CPU's caches) and returns a
+// Share whose Data aliases the arena (valid until Reset).
+func (a *Arena) Put(number int, data []byte) (Share, error) {
+	var p unsafe.Pointer
+	if len(data) > 0 {
+		p = unsafe.Pointer(&data[0])
+	}
+	slot := C.rs_arena_put(a.a, p, C.size_t(len(data)))
+	if slot == nil {
+		return Share{}, errors.New("infectious: arena full")
+	}
+	return Share{Number: number, Data: unsafe.Slice((*byte)(slot), len(data))}, nil
+}
+
 // UnmarshalShard parses a wire erasurecode.Shard (protobuf/shard.proto:21-27)
 // and places ShardData in the arena -- the one copy gogo's Unmarshal makes
 // anyway (shard.pb.go:468-503).  The returned Share's Data aliases the arena

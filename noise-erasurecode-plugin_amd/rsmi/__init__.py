@@ -43,7 +43,7 @@ EXPORTS = (
     "rs_pinned_alloc", "rs_pinned_free", "rs_device_alloc", "rs_device_free",
     "rs_stream_sync", "rs_fill_splitmix", "rs_kernel_name",
     "rs_blake2b_batch", "rs_blake2b_device", "rs_blake2b", "rs_blake2b_host",
-    "rs_stat", "rs_arena_new", "rs_arena_alloc", "rs_arena_reset", "rs_arena_used", "rs_arena_free",
+    "rs_stat", "rs_arena_new", "rs_arena_alloc", "rs_arena_put", "rs_arena_reset", "rs_arena_used", "rs_arena_free",
     "rs_new_devices", "rs_member_count", "rs_member", "rs_partition",
     "rs_encode_stripes_parts", "rs_reconstruct_stripes_parts", "rs_reconstruct_spread",
 )
@@ -114,6 +114,7 @@ def _lib() -> ctypes.CDLL:
             "rs_stat": (ctypes.c_int64, [vp, i32]),
             "rs_arena_new": (vp, [sz]),
             "rs_arena_alloc": (vp, [vp, sz]),
+            "rs_arena_put": (vp, [vp, vp, sz]),
             "rs_arena_reset": (None, [vp]),
             "rs_arena_used": (sz, [vp]),
             "rs_arena_free": (None, [vp]),
@@ -481,12 +482,12 @@ class Arena:
             raise RSError(RS_ENOMEM, "rs_arena_new")
 
     def put(self, data: bytes) -> int:
-        """Copies data into a fresh 16-byte aligned slot; returns its address."""
-        p = _lib().rs_arena_alloc(self._a, len(data))
+        """Copies data into a fresh 16-byte aligned slot (rs_arena_put:
+        streaming stores, as rs_shard_unmarshal_arena); returns its address."""
+        buf = bytes(data)
+        p = _lib().rs_arena_put(self._a, buf, len(buf))
         if not p:
-            raise RSError(RS_ENOMEM, "rs_arena_alloc")
-        if data:
-            ctypes.memmove(p, bytes(data), len(data))
+            raise RSError(RS_ENOMEM, "rs_arena_put")
         return p
 
     def used(self) -> int:

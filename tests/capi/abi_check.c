@@ -141,6 +141,12 @@ static void check_arena_batch(rs_ctx *ctx, int k, int n, size_t S, int B) {
     CHECK(rs_stat(ctx, RS_STAT_BATCHES_IN_PLACE) == in_place0 + rs_member_count(ctx), "batch not read in place");
     for (int b = 0; b < B; b++) { free(inputs[b]); free(dsts[b]); }
     free(inputs); free(dsts); free(counts); free(nums); free(st); free(ptrs);
+    /* rs_arena_put: a copy in a fresh aligned slot; NULL once the arena is full */
+    rs_arena_reset(arena);
+    const char msg[] = "arena put";
+    void *slot = rs_arena_put(arena, msg, sizeof msg);
+    CHECK(slot != NULL && ((uintptr_t)slot & 15u) == 0 && memcmp(slot, msg, sizeof msg) == 0, "rs_arena_put");
+    CHECK(rs_arena_put(arena, msg, (size_t)1 << 40) == NULL, "rs_arena_put past the end");
     rs_arena_free(arena);
 }
 
