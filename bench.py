@@ -105,7 +105,7 @@ def parse():
     ap.add_argument("--no-extra-legs", dest="extra_legs", action="store_false",
                     help="N = 1: skip the configs[0] (per-message latency), configs[4] (RS(64,16)) and "
                          "configs[2] worst-case legs reported beside the headline")
-    ap.add_argument("--config1-reps", type=int, default=50)
+    ap.add_argument("--config1-reps", type=int, default=200)
     ap.add_argument("--config5-stripes", type=int, default=16384)
     ap.add_argument("--config5-steps", type=int, default=5)
     ap.add_argument("--config5-warmup", type=int, default=2)
