@@ -133,3 +133,11 @@ def test_mailbox_grid_gives_up_and_caller_recovers():
     # chunks are staged, and the caller launches them itself -- same bytes.
     calls, mb, rec = _child(RSMI_MAILBOX_TIMEOUT_US="1")
     assert mb == calls and rec > 0
+
+
+@pytest.mark.parametrize("split", ["50", "20,45,75"])
+def test_mailbox_other_chunk_splits(split):
+    # Two and four column chunks (RSMI_CHUNK_SPLIT): a group per chunk, the
+    # same bytes.
+    calls, mb, rec = _child(RSMI_CHUNK_SPLIT=split)
+    assert mb == calls and rec == 0
