@@ -23,7 +23,7 @@ import numpy as np  # noqa: E402
 import rsmi  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-what = sys.argv[1]  # encode | decode | encode_batch | decode_batch (64 messages per call)
+what = sys.argv[1]  # encode | decode | decode_arena | encode_batch | decode_batch (64 messages per call)
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
 k, n = 10, 14
 m = n - k
@@ -43,6 +43,9 @@ ptrs = (ctypes.c_void_p * k)(*[b.ctypes.data for b in bufs])
 dst = np.zeros(L, dtype=np.uint8)
 bp, pp, dp = P(blob.ctypes.data), P(parity.ctypes.data), P(dst.ctypes.data)
 B = 64
+if what == "decode_arena":  # the survivors in an engine-pinned rs_arena (read in place)
+    arena = rsmi.Arena(k * (S + 256) + 4096)
+    ptrs = (ctypes.c_void_p * k)(*[arena.put(b.tobytes()) for b in bufs])
 if what.endswith("batch"):
     reps = max(5, reps // 20)
     rng = np.random.default_rng(0xBA7C)
@@ -63,14 +66,14 @@ for _ in range(reps):
     t0 = time.perf_counter()
     if what == "encode":
         lib.rs_encode(f.handle, bp, L, pp)
-    elif what == "decode":
+    elif what in ("decode", "decode_arena"):
         lib.rs_decode(f.handle, nums, ptrs, k, S, dp)
     elif what == "encode_batch":
         lib.rs_encode_batch(f.handle, B, eins, L, eout, bst)
     else:
         lib.rs_decode_batch(f.handle, B, bcounts, bnums, bptrs, S, bout, bst)
     ts.append(time.perf_counter() - t0)
-if what == "decode":
+if what in ("decode", "decode_arena"):
     assert np.array_equal(dst, blob)
 if what == "decode_batch":
     assert all(np.array_equal(d, blob) for d in bdst)
