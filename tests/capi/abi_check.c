@@ -223,6 +223,10 @@ int main(void) {
         return 2;
     }
     check_encode_decode(c10, 10, 14, 1048580, 0x5EED); /* BASELINE config 1 */
+    /* a config-1 message's encode and decode go through the mailbox grid
+     * (unless RSMI_MAILBOX=0), and no chunk was left to the caller */
+    if (!getenv("RSMI_MAILBOX"))
+        CHECK(rs_stat(c10, RS_STAT_MAILBOX_CALLS) >= 2 && rs_stat(c10, RS_STAT_MAILBOX_RECOVERED) == 0, "mailbox grid");
     check_encode_decode(c10, 10, 14, 10 * 17, 3);
     check_encode_decode(c64, 64, 80, 64 * 4099, 4);
     check_encode_decode(c4, 4, 6, 64, 5);              /* plugin default RS(4,2) */
